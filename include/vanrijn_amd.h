@@ -1,0 +1,255 @@
+/*
+ * vanrijn_amd.h -- C ABI of the MI355X (gfx950) path-tracing core.
+ *
+ * Drop-in boundary for vanrijn's per-pixel hot path.  The reference's boundary is
+ *     pub fn partial_render_scene(scene: &Scene, tile: Tile, height: usize, width: usize)
+ *         -> AccumulationBuffer                                   (src/camera.rs:95-130)
+ * called concurrently from rayon workers in src/main.rs:204 and from benches/simple_scene.rs:45.
+ * Every entry point below names the reference interface it replaces.  Plain pointers and sizes
+ * only; no HIP or torch types in the signatures (streams are passed as void*).  A Rust binding
+ * (extern "C" block) is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All floating point is IEEE binary64, as in the reference (everything on the path is f64).
+ *   - Return value: VR_OK (0) or a negative vr_status.  The message of the last failure on the
+ *     calling thread is in vr_last_error().  Nothing unwinds across the ABI; where the reference
+ *     panics (singular shading basis, out-of-range tile) the call returns an error instead.
+ *   - A vr_scene is immutable after creation and may be shared by any number of threads;
+ *     render calls are re-entrant (each call uses its own stream and scratch).
+ */
+#ifndef VANRIJN_AMD_H
+#define VANRIJN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_ABI_VERSION 1
+#define VR_MAX_SPECTRUM_SAMPLES 64
+#define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
+
+typedef enum vr_status {
+    VR_OK = 0,
+    VR_ERROR_INVALID_ARGUMENT = -1,
+    VR_ERROR_OUT_OF_MEMORY = -2,
+    VR_ERROR_DEVICE = -3,          /* a HIP call failed */
+    VR_ERROR_NO_DEVICE = -4,       /* no gfx950 device visible */
+    VR_ERROR_SINGULAR_BASIS = -5,  /* simple_random_integrator.rs:26-31 would panic ("expect") */
+    VR_ERROR_IO = -6,              /* load_obj: std::io::Error (src/mesh.rs:74-77) */
+    VR_ERROR_UNSUPPORTED = -7,     /* e.g. BVH deeper than the traversal stack */
+    VR_ERROR_HOST_ONLY = -8        /* render call on a scene created with VR_SCENE_HOST_ONLY */
+} vr_status;
+
+typedef struct vr_vec3 {
+    double x, y, z;
+} vr_vec3; /* math::Vec3 (src/math/vec3.rs:8-10) */
+
+/* colour::Spectrum (src/colour/spectrum.rs:5-10): samples linearly interpolated over
+ * [shortest_wavelength, longest_wavelength], zero outside. */
+typedef struct vr_spectrum {
+    double shortest_wavelength;
+    double longest_wavelength;
+    uint32_t sample_count; /* 2 .. VR_MAX_SPECTRUM_SAMPLES */
+    const double* samples;
+} vr_spectrum;
+
+typedef enum vr_material_kind {
+    VR_MATERIAL_LAMBERTIAN = 0, /* materials/lambertian_material.rs:12-60 */
+    VR_MATERIAL_REFLECTIVE = 1  /* materials/reflective_material.rs:8-48 */
+} vr_material_kind;
+
+typedef struct vr_material_desc {
+    int32_t kind;
+    uint32_t reserved;
+    vr_spectrum colour;
+    double diffuse_strength;
+    double reflection_strength; /* reflective only */
+} vr_material_desc;
+
+typedef enum vr_primitive_kind {
+    VR_PRIMITIVE_PLANE = 0, /* raycasting/plane.rs:18-31: vector = normal (normalised here, as Plane::new), scalar = distance_from_origin */
+    VR_PRIMITIVE_SPHERE = 1 /* raycasting/sphere.rs:15-23: vector = centre, scalar = radius */
+} vr_primitive_kind;
+
+typedef struct vr_primitive_desc {
+    int32_t kind;
+    uint32_t material;
+    vr_vec3 vector;
+    double scalar;
+} vr_primitive_desc;
+
+/* A triangle mesh (Vec<Arc<dyn Primitive>> of raycasting::Triangle, src/raycasting/triangle.rs:8-13).
+ * vertices/normals: [triangle][corner 0..2][xyz] doubles; copied by vr_scene_create. */
+typedef struct vr_mesh_desc {
+    uint64_t triangle_count;
+    const double* vertices;
+    const double* normals;
+    uint32_t material;
+    uint32_t reserved;
+} vr_mesh_desc;
+
+typedef enum vr_object_kind {
+    VR_OBJECT_PRIMITIVE_LIST = 0, /* Box<Vec<Box<dyn Primitive>>> (raycasting/vec_aggregate.rs:11-24) */
+    VR_OBJECT_BVH = 1             /* Box<BoundingVolumeHierarchy> (raycasting/bounding_volume_hierarchy.rs:49-74) */
+} vr_object_kind;
+
+typedef struct vr_object_desc {
+    int32_t kind;
+    uint32_t first; /* primitive list: first primitive index; BVH: mesh index */
+    uint32_t count; /* primitive list: number of primitives; BVH: must be 1 */
+    uint32_t reserved;
+} vr_object_desc;
+
+/* scene::Scene (src/scene.rs:5-8): camera_location + objects in order (order decides ties,
+ * sampler.rs:9-20). */
+typedef struct vr_scene_desc {
+    vr_vec3 camera_location;
+    uint32_t material_count;
+    uint32_t primitive_count;
+    uint32_t mesh_count;
+    uint32_t object_count;
+    const vr_material_desc* materials;
+    const vr_primitive_desc* primitives;
+    const vr_mesh_desc* meshes;
+    const vr_object_desc* objects;
+} vr_scene_desc;
+
+typedef struct vr_scene vr_scene;
+
+#define VR_SCENE_HOST_ONLY 1u /* build + flatten only, no device upload (inspection, CPU tests) */
+
+/* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
+ * Copies every input; builds one BVH per mesh with the reference's median split
+ * (bounding_volume_hierarchy.rs:38-74; ties in the sort broken by input triangle index);
+ * flattens it and uploads it to `device` (HIP ordinal). */
+int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, vr_scene** out);
+void vr_scene_destroy(vr_scene* scene);
+
+typedef struct vr_scene_info {
+    uint64_t triangle_count;
+    uint64_t node_count;     /* flattened interior nodes over all BVHs */
+    uint32_t max_bvh_depth;  /* levels, root = 1 */
+    uint32_t object_count;
+    double extent;           /* max |coordinate| of camera and geometry */
+    uint64_t device_bytes;   /* scene bytes resident in HBM */
+} vr_scene_info;
+int vr_scene_get_info(const vr_scene* scene, vr_scene_info* out);
+/* BVH leaf (in-order) sequence of mesh `mesh`: out[i] = input triangle index of leaf i. */
+int vr_scene_bvh_leaf_order(const vr_scene* scene, uint32_t mesh, uint64_t* out);
+
+/* util::Tile (src/util/tile_iterator.rs:1-7): half-open row/column ranges of the full image. */
+typedef struct vr_tile {
+    uint64_t start_column, end_column, start_row, end_row;
+} vr_tile;
+
+/* AccumulationBuffer (src/accumulation_buffer.rs:6-12), row-major over the tile:
+ * colour/colour_sum/colour_bias: [height][width][3] XYZ; weight/weight_bias: [height][width].
+ * colour is the running mean (sum * (1/weight)); the *_bias arrays are the Kahan compensation. */
+typedef struct vr_accumulation_buffer {
+    uint64_t width, height;
+    double* colour;
+    double* colour_sum;
+    double* colour_bias;
+    double* weight;
+    double* weight_bias;
+} vr_accumulation_buffer;
+
+/* Sampling parameters.  Each (pixel, sample) draws its random numbers from the counter-based
+ * stream (seed, row*width+column, first_sample + s) ("vr-splitmix v1"), so results do
+ * not depend on tiling, launch split or device count. */
+typedef struct vr_render_params {
+    vr_tile tile;
+    uint64_t height, width; /* full image, as partial_render_scene's height/width */
+    uint32_t spp;           /* samples per pixel in this call (partial_render_scene == 1) */
+    uint32_t accumulate;    /* 0: start from AccumulationBuffer::new(); 1: continue update_pixel */
+    uint64_t seed;
+    uint64_t first_sample;
+} vr_render_params;
+
+/* Replaces partial_render_scene (camera.rs:95-130) one-for-one: one sample per pixel into a
+ * fresh tile buffer (`out` arrays are caller-allocated host memory, tile-sized).  The sample
+ * index comes from a per-scene atomic pass counter, so concurrent callers get distinct random
+ * streams like the reference's thread_rng.  Thread-safe. */
+int vr_partial_render_scene(const vr_scene* scene, vr_tile tile, uint64_t height, uint64_t width,
+                            vr_accumulation_buffer* out);
+
+/* Generalised form: spp samples per pixel, explicit seed / sample range, host buffers; `buf`
+ * is read first when params->accumulate is 1 (update_pixel continuation). */
+int vr_render_tile(const vr_scene* scene, const vr_render_params* params, vr_accumulation_buffer* buf);
+
+/* Device-resident form for the multi-GPU path: `state` is a device pointer to
+ * tile_width*tile_height records of 8 doubles {sum X, sum Y, sum Z, bias X, bias Y, bias Z,
+ * weight, weight_bias} on the scene's device; `stream` is a hipStream_t (NULL = the scene's own
+ * stream) and the call only enqueues work (no host synchronisation). */
+typedef struct vr_launch_stats {
+    float kernel_ms;          /* HIP-event time of the render kernel(s), valid when timed != 0 */
+    uint32_t timed;
+    uint64_t box_tests;       /* filled only when counters were requested */
+    uint64_t node_visits;
+    uint64_t triangle_tests;
+    uint64_t rays;
+    uint64_t shaded_triangle_hits;
+    uint64_t samples;
+} vr_launch_stats;
+
+#define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */
+#define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
+
+int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
+                          uint32_t launch_flags, vr_launch_stats* stats);
+/* Mean XYZ of host-side state records: colour = colour_sum * (1 / weight)
+ * (accumulation_buffer.rs:59).  States of disjoint sample sets (e.g. one per GPU) merge by
+ * element-wise addition of the 8-double records (the cross-GPU reduce), which is what
+ * AccumulationBuffer::merge_tile's weighted blend (accumulation_buffer.rs:62-85) computes. */
+int vr_resolve_state(const double* state_host, uint64_t pixel_count, double* colour_out);
+
+/* Per-(pixel, sample) records, for decision-identity checks against the oracle. */
+typedef struct vr_sample_record {
+    double wavelength; /* final photon wavelength (0 on camera miss / recursion limit) */
+    double intensity;  /* final photon intensity before the x360 pdf scale */
+    double xyz[3];     /* ColourXyz::from_photon of the scaled photon */
+    int32_t bounces;   /* bounce rays traced */
+    int32_t flags;     /* bit0 camera ray hit, bit1 recursion limit reached, bit2 singular basis */
+} vr_sample_record;
+int vr_render_samples(const vr_scene* scene, const vr_render_params* params, vr_sample_record* out);
+
+/* Sampler::sample (src/sampler.rs:9-20) for a batch of rays (origins/directions: [n][3], the
+ * directions are used as given, as Ray's fields).  Host arrays. */
+typedef struct vr_hit_record {
+    int32_t valid;
+    int32_t object;
+    int64_t primitive; /* primitive-list position, or BVH leaf position */
+    double distance;
+    double location[3];
+    double normal[3];
+    double tangent[3];
+    double cotangent[3];
+    double retro[3];
+} vr_hit_record;
+int vr_trace_rays(const vr_scene* scene, uint64_t n, const double* origins, const double* directions,
+                  vr_hit_record* out);
+
+/* Host helpers (scene setup; no device work). */
+/* Spectrum::reflection_from_linear_rgb (spectrum.rs:81-165): 32 samples over [380, 720] nm. */
+int vr_spectrum_reflection_from_linear_rgb(double red, double green, double blue, double out[32]);
+/* Spectrum::intensity_at_wavelength (spectrum.rs:64-79). */
+double vr_spectrum_intensity_at_wavelength(const vr_spectrum* spectrum, double wavelength);
+/* ColourXyz::for_wavelength (colour_xyz.rs:22-29). */
+void vr_colour_xyz_for_wavelength(double wavelength, double out[3]);
+/* mesh::load_obj (src/mesh.rs:74-88): positions/normals parsed as f32 then widened, polygons
+ * fan-triangulated; missing normals are zero.  Returns a malloc'ed [n][3][3] pair; free with
+ * vr_mesh_free. */
+int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, double** normals);
+void vr_mesh_free(double* vertices, double* normals);
+
+int vr_device_count(void);
+const char* vr_last_error(void);
+uint32_t vr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VANRIJN_AMD_H */

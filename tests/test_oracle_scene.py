@@ -1,0 +1,141 @@
+"""Oracle scene-level self-consistency and host-side agreement with the product (CPU only).
+
+* The product's host BVH build (C++, vr_scene_create with VR_SCENE_HOST_ONLY) and the oracle's
+  restatement of BoundingVolumeHierarchy::build produce the same leaf order (the tie rule of the
+  traversal depends on it).
+* The oracle's pruned traversal (the culling rule the GPU kernel uses) returns exactly the
+  reference-mode (exhaustive) closest hit on camera rays, bounce rays and random rays.
+* The product's host helpers (Spectrum::reflection_from_linear_rgb, intensity_at_wavelength,
+  ColourXyz::for_wavelength) are bit-identical to the oracle's.
+"""
+import numpy as np
+import pytest
+
+from vanrijn_amd import scenes
+from vanrijn_amd.render import Tile
+
+
+@pytest.fixture(scope="module")
+def small_mesh():
+    return scenes.displaced_mesh(12, scenes._BUNNY_BUMPS, 0xB0BB1E, 12, 0.04, (0.95, 0.80, 0.90), (-1.2, -1.05, -0.1))
+
+
+@pytest.fixture(scope="module")
+def bunny():
+    return scenes.procedural_bunny()
+
+
+def test_procedural_bunny_is_deterministic(bunny):
+    v, n = scenes.procedural_bunny()
+    assert np.array_equal(v, bunny[0]) and np.array_equal(n, bunny[1])
+    assert v.shape == (69312, 3, 3)
+    assert np.isfinite(v).all() and np.isfinite(n).all()
+
+
+def test_bvh_leaf_order_matches_oracle(oracle, bunny):
+    for scene in (scenes.main_scene(bunny), scenes.bench_scene(bunny)):
+        spec = scene.spec()
+        ds = scene.device_scene(0, host_only=True)
+        orc = oracle.OracleScene(spec)
+        obj = [i for i, o in enumerate(spec.objects) if o.kind == "bvh"][0]
+        assert np.array_equal(ds.leaf_order(0).astype(np.int64), orc.leaf_order(obj))
+        assert ds.info()["max_bvh_depth"] == orc.depth(obj)
+
+
+def test_spectrum_helpers_match_oracle(oracle):
+    from vanrijn_amd.scene import ColourRgbF, Spectrum
+    g = np.random.default_rng(3)
+    for _ in range(200):
+        r, gg, b = g.uniform(-0.5, 1.5, 3)
+        if g.random() < 0.3:
+            gg = r
+        s = Spectrum.reflection_from_linear_rgb(ColourRgbF(r, gg, b))
+        assert np.array_equal(s.samples, oracle.reflection_from_linear_rgb(r, gg, b))
+        for wl in g.uniform(370, 750, 5):
+            assert s.intensity_at_wavelength(wl) == oracle.spectrum_intensity(380.0, 720.0, s.samples, wl)
+    import ctypes as C
+    from vanrijn_amd import _native as N
+    out = np.zeros(3)
+    for wl in np.concatenate([[0.0, 380.0, 500.0, 740.0], g.uniform(300, 800, 50)]):
+        N.lib().vr_colour_xyz_for_wavelength(wl, out.ctypes.data_as(C.c_void_p))
+        assert np.array_equal(out, oracle.xyz_for_wavelength(wl))
+
+
+def _rays(scene_spec, n, seed):
+    g = np.random.default_rng(seed)
+    cam = np.array(scene_spec.camera_location)
+    # camera-like rays towards the mesh region, and random rays from random points
+    tgt = g.uniform([-2.5, -2.0, -1.5], [0.0, 0.6, 1.0], (n, 3))
+    d1 = tgt - cam
+    o2 = g.uniform([-3.0, -2.0, -1.5], [0.5, 1.0, 1.0], (n, 3))
+    d2 = g.normal(size=(n, 3))
+    o = np.concatenate([np.repeat(cam[None], n, 0), o2])
+    d = np.concatenate([d1, d2])
+    d = d / np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d
+
+
+def _same_hits(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert x.valid == y.valid
+        if x.valid:
+            assert (x.object, x.primitive) == (y.object, y.primitive)
+            assert x.distance == y.distance
+            assert list(x.normal) == list(y.normal) or (np.isnan(x.normal[:]).all() and np.isnan(y.normal[:]).all())
+
+
+def test_pruned_traversal_equals_exhaustive_on_rays(oracle, small_mesh):
+    scene = scenes.main_scene(small_mesh)
+    orc = oracle.OracleScene(scene.spec())
+    o, d = _rays(scene.spec(), 1500, 5)
+    ref, cref = orc.trace(o, d, oracle.MODE_REFERENCE)
+    prn, cprn = orc.trace(o, d, oracle.MODE_PRUNED)
+    _same_hits(ref, prn)
+    assert cprn["box_tests"] < cref["box_tests"]
+
+
+def test_pruned_render_equals_exhaustive(oracle, small_mesh):
+    for scene in (scenes.main_scene(small_mesh), scenes.bench_scene(small_mesh)):
+        orc = oracle.OracleScene(scene.spec())
+        t = Tile(8, 40, 10, 42)
+        a = orc.render_samples(t, 48, 48, 3, seed=11, mode=oracle.MODE_REFERENCE)
+        b = orc.render_samples(t, 48, 48, 3, seed=11, mode=oracle.MODE_PRUNED)
+        assert np.array_equal(a["bounces"], b["bounces"])
+        assert np.array_equal(a["flags"], b["flags"])
+        assert np.array_equal(a["wavelength"], b["wavelength"])
+        assert np.array_equal(a["intensity"], b["intensity"])
+        assert (a["flags"] & 1).sum() > 0  # the mesh is in view
+
+
+@pytest.mark.slow
+def test_pruned_render_equals_exhaustive_full_bunny(oracle, bunny):
+    scene = scenes.main_scene(bunny)
+    orc = oracle.OracleScene(scene.spec())
+    t = Tile(60, 76, 70, 86)
+    a = orc.render_samples(t, 128, 128, 2, seed=3, mode=oracle.MODE_REFERENCE, nthreads=8)
+    b = orc.render_samples(t, 128, 128, 2, seed=3, mode=oracle.MODE_PRUNED, nthreads=8)
+    assert np.array_equal(a["bounces"], b["bounces"])
+    assert np.array_equal(a["intensity"], b["intensity"])
+
+
+def test_oracle_render_tile_invariance(oracle, small_mesh):
+    """Random streams are keyed by global pixel index: tiles reproduce the full frame exactly."""
+    scene = scenes.main_scene(small_mesh)
+    orc = oracle.OracleScene(scene.spec())
+    full = orc.render_tile(Tile(0, 24, 0, 20), 20, 24, 2, seed=9, mode=oracle.MODE_PRUNED)
+    part = orc.render_tile(Tile(5, 17, 3, 11), 20, 24, 2, seed=9, mode=oracle.MODE_PRUNED)
+    assert np.array_equal(full["colour_sum"][3:11, 5:17], part["colour_sum"])
+    assert np.array_equal(full["weight"], np.full((20, 24), 2.0))
+
+
+def test_oracle_accumulate_continuation(oracle, small_mesh):
+    scene = scenes.bench_scene(small_mesh)
+    orc = oracle.OracleScene(scene.spec())
+    t = Tile(0, 16, 0, 16)
+    once = orc.render_tile(t, 16, 16, 4, seed=2, mode=oracle.MODE_PRUNED)
+    two = orc.render_tile(t, 16, 16, 2, seed=2, mode=oracle.MODE_PRUNED)
+    two = orc.render_tile(t, 16, 16, 2, seed=2, first_sample=2, mode=oracle.MODE_PRUNED,
+                          accumulate={k: v for k, v in two.items() if k != "counters"})
+    for k in ("colour", "colour_sum", "colour_bias", "weight", "weight_bias"):
+        assert np.array_equal(once[k], two[k])

@@ -1,0 +1,796 @@
+// vr_host.cpp -- host side of the MI355X path-tracing core: scene construction (copy, the
+// reference's median-split BVH build, flattening to the 128-B node layout, HBM upload) and the
+// extern "C" entry points declared in include/vanrijn_amd.h.
+//
+// Reference interfaces replaced here:
+//   Scene { camera_location, objects }            src/scene.rs:5-8
+//   BoundingVolumeHierarchy::build                src/raycasting/bounding_volume_hierarchy.rs:38-74
+//   Plane::new                                    src/raycasting/plane.rs:18-31
+//   partial_render_scene                          src/camera.rs:95-130
+//   AccumulationBuffer::{new, update_pixel}       src/accumulation_buffer.rs:14-60
+//   Spectrum::reflection_from_linear_rgb / intensity_at_wavelength   src/colour/spectrum.rs:64-165
+//   ColourXyz::for_wavelength                     src/colour/colour_xyz.rs:22-29, 86-103
+//   load_obj                                      src/mesh.rs:13-88
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vanrijn_amd.h"
+#include "rgb_spectrum_tables.h"
+#include "vr_layout.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define VR_HIP(call)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(VR_ERROR_DEVICE, std::string(#call " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// Host math in the reference's operation order (only what scene setup needs)
+// ------------------------------------------------------------------------------------------
+struct H3 {
+    double x, y, z;
+};
+double hdot(H3 a, H3 b) {
+    double s = -0.0;  // `Sum for f64` folds from -0.0 (vec3.rs:76-82)
+    s = s + a.x * b.x;
+    s = s + a.y * b.y;
+    s = s + a.z * b.z;
+    return s;
+}
+H3 hcross(H3 a, H3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+H3 hnormalize(H3 a) {
+    double inv = 1.0 / std::sqrt(hdot(a, a));
+    return {a.x * inv, a.y * inv, a.z * inv};
+}
+
+// ------------------------------------------------------------------------------------------
+// BVH build (bounding_volume_hierarchy.rs:30-74) and flattening
+// ------------------------------------------------------------------------------------------
+struct Interval {  // util/interval.rs
+    double min, max;
+};
+Interval iv_empty() { return {INFINITY, -INFINITY}; }
+bool iv_is_empty(Interval a) { return a.min > a.max; }
+Interval iv_union(Interval a, Interval b) {  // interval.rs:66-77 (f64::min/max ignore NaN)
+    if (iv_is_empty(a)) return b;
+    if (iv_is_empty(b)) return a;
+    return {std::fmin(a.min, b.min), std::fmax(a.max, b.max)};
+}
+Interval iv_expand(Interval a, double v) {  // interval.rs:79-87
+    if (iv_is_empty(a)) return {v, v};
+    return {std::fmin(a.min, v), std::fmax(a.max, v)};
+}
+struct Box3 {
+    Interval b[3];
+};
+Box3 box_empty() { return {{iv_empty(), iv_empty(), iv_empty()}}; }
+Box3 box_union(const Box3& a, const Box3& b) {
+    return {{iv_union(a.b[0], b.b[0]), iv_union(a.b[1], b.b[1]), iv_union(a.b[2], b.b[2])}};
+}
+int largest_dimension(const Box3& bb) {  // util/axis_aligned_bounding_box.rs:76-99
+    int acc = 0;
+    double acc_size = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        double size = bb.b[i].min == bb.b[i].max ? -1.0 : bb.b[i].max - bb.b[i].min;
+        if (size > acc_size) {
+            acc = i;
+            acc_size = size;
+        }
+    }
+    return acc;
+}
+void box_to_layout(const Box3& bb, double out[6]) {
+    for (int i = 0; i < 3; ++i) {
+        out[2 * i] = bb.b[i].min;
+        out[2 * i + 1] = bb.b[i].max;
+    }
+}
+
+struct BuildPrim {
+    Box3 box;
+    double centre[3];
+    uint64_t orig;
+};
+
+struct BvhBuilder {
+    std::vector<BuildPrim> prims;  // permuted in place into leaf order
+    std::vector<vr::Node> nodes;   // interior nodes, preorder
+    int max_depth = 0;
+    int tri_base = 0;
+
+    // Returns the child encoding of the subtree over prims[lo, hi): >= 0 interior node index,
+    // < 0 leaf ~(tri_base + leaf position).  `bounds` receives the subtree's box.
+    int32_t build(uint64_t lo, uint64_t hi, int level, Box3& bounds) {
+        max_depth = std::max(max_depth, level + 1);
+        bounds = box_empty();
+        for (uint64_t i = lo; i < hi; ++i) bounds = box_union(bounds, prims[i].box);
+        if (hi - lo <= 1) return ~(int32_t)(tri_base + lo);
+        const int axis = largest_dimension(bounds);
+        // sort_unstable_by(centre[axis].partial_cmp, NaN -> Equal); equal keys ordered by input
+        // index so the permutation is unique (the oracle applies the same rule)
+        std::sort(prims.begin() + lo, prims.begin() + hi, [axis](const BuildPrim& a, const BuildPrim& b) {
+            double ca = a.centre[axis], cb = b.centre[axis];
+            if (ca < cb) return true;
+            if (ca > cb) return false;
+            return a.orig < b.orig;
+        });
+        const uint64_t pivot = (hi - lo) / 2;
+        const int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box3 lb, rb;
+        int32_t l = build(lo, lo + pivot, level + 1, lb);
+        int32_t r = build(lo + pivot, hi, level + 1, rb);
+        vr::Node& n = nodes[me];
+        std::memset(&n, 0, sizeof n);
+        box_to_layout(lb, n.box[0]);
+        box_to_layout(rb, n.box[1]);
+        n.child[0] = l;
+        n.child[1] = r;
+        return me;
+    }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Scene
+// ------------------------------------------------------------------------------------------
+struct vr_scene {
+    int device = -1;
+    bool host_only = false;
+    double camera[3];
+    double extent = 0.0;
+    std::vector<vr::Material> materials;
+    std::vector<vr::Prim> prims;
+    std::vector<vr::Bvh> bvhs;
+    std::vector<vr::Node> nodes;
+    std::vector<vr::TriVerts> tris;
+    std::vector<vr::TriNormals> normals;
+    std::vector<std::vector<uint64_t>> leaf_order;  // per mesh
+    std::vector<int> mesh_tri_base;
+    int max_depth = 0;
+    uint32_t object_count = 0;
+    // device copies
+    void* d_block = nullptr;
+    size_t device_bytes = 0;
+    vr::DeviceScene dev{};
+    int32_t* d_error = nullptr;
+    unsigned long long* d_counters = nullptr;
+    std::mutex counter_mutex;
+    std::atomic<uint64_t> pass_counter{0};
+    uint64_t partial_seed = 0x5EED0001ull;
+};
+
+namespace {
+
+int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }
+
+template <class T>
+size_t align_up(size_t v) {
+    return (v + 255) & ~size_t(255);
+}
+
+int upload(vr_scene* s) {
+    VR_HIP(hipSetDevice(s->device));
+    const size_t sz_nodes = s->nodes.size() * sizeof(vr::Node);
+    const size_t sz_tris = s->tris.size() * sizeof(vr::TriVerts);
+    const size_t sz_norm = s->normals.size() * sizeof(vr::TriNormals);
+    const size_t sz_mat = s->materials.size() * sizeof(vr::Material);
+    const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
+    const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
+    size_t off[7], total = 0;
+    const size_t sizes[7] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh, 64 + 8 * sizeof(unsigned long long)};
+    for (int i = 0; i < 7; ++i) {
+        off[i] = total;
+        total += align_up<char>(std::max<size_t>(sizes[i], 1));
+    }
+    VR_HIP(hipMalloc(&s->d_block, total));
+    s->device_bytes = total;
+    char* base = (char*)s->d_block;
+    const void* src[6] = {s->nodes.data(), s->tris.data(), s->normals.data(), s->materials.data(), s->prims.data(),
+                          s->bvhs.data()};
+    for (int i = 0; i < 6; ++i)
+        if (sizes[i]) VR_HIP(hipMemcpy(base + off[i], src[i], sizes[i], hipMemcpyHostToDevice));
+    VR_HIP(hipMemset(base + off[6], 0, sizes[6]));
+    s->d_error = (int32_t*)(base + off[6]);
+    s->d_counters = (unsigned long long*)(base + off[6] + 64);
+    vr::DeviceScene& d = s->dev;
+    d.nodes = (const vr::Node*)(base + off[0]);
+    d.tris = (const vr::TriVerts*)(base + off[1]);
+    d.normals = (const vr::TriNormals*)(base + off[2]);
+    d.materials = (const vr::Material*)(base + off[3]);
+    d.prims = (const vr::Prim*)(base + off[4]);
+    d.bvhs = (const vr::Bvh*)(base + off[5]);
+    return VR_OK;
+}
+
+int check_render_params(const vr_scene* s, const vr_render_params* p) {
+    if (!s || !p) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene or params");
+    if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
+    const vr_tile& t = p->tile;
+    // Tile and Array2D index asserts in the reference (array2d.rs:58,65) panic; here: an error
+    if (t.end_column < t.start_column || t.end_row < t.start_row || t.end_column > p->width ||
+        t.end_row > p->height || p->width == 0 || p->height == 0)
+        return fail(VR_ERROR_INVALID_ARGUMENT, "tile outside the image");
+    if (stack_depth(s) > 48) return fail(VR_ERROR_UNSUPPORTED, "BVH deeper than the largest traversal stack (48)");
+    return VR_OK;
+}
+
+vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* state) {
+    vr::RenderArgs a{};
+    a.scene = s->dev;
+    a.start_column = p->tile.start_column;
+    a.start_row = p->tile.start_row;
+    a.tile_width = p->tile.end_column - p->tile.start_column;
+    a.tile_height = p->tile.end_row - p->tile.start_row;
+    a.width = p->width;
+    a.height = p->height;
+    a.seed = p->seed;
+    a.first_sample = p->first_sample;
+    a.spp = p->spp;
+    a.accumulate = p->accumulate;
+    a.state = state;
+    a.records = nullptr;
+    a.counters = nullptr;
+    a.error_flag = s->d_error;
+    return a;
+}
+
+int read_and_clear_error(const vr_scene* s, hipStream_t stream) {
+    int32_t flag = 0;
+    VR_HIP(hipMemcpyAsync(&flag, s->d_error, sizeof flag, hipMemcpyDeviceToHost, stream));
+    VR_HIP(hipStreamSynchronize(stream));
+    if (flag) {
+        VR_HIP(hipMemsetAsync(s->d_error, 0, sizeof flag, stream));
+        VR_HIP(hipStreamSynchronize(stream));
+        return fail(VR_ERROR_SINGULAR_BASIS,
+                    "Normal, tangent and cotangent don't form a valid basis (det == 0); the reference panics here");
+    }
+    return VR_OK;
+}
+
+// RAII device buffer + stream for the synchronous host-buffer entry points
+struct CallScratch {
+    hipStream_t stream = nullptr;
+    void* ptr = nullptr;
+    ~CallScratch() {
+        if (ptr) (void)hipFree(ptr);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+uint32_t vr_abi_version(void) { return VR_ABI_VERSION; }
+
+const char* vr_last_error(void) { return g_last_error.c_str(); }
+
+int vr_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int vr_spectrum_reflection_from_linear_rgb(double red, double green, double blue, double out[32]) {
+    if (!out) return fail(VR_ERROR_INVALID_ARGUMENT, "null output");
+    const double r = red, g = green, b = blue;
+    double c0, c1, c2;
+    int kx, ky;
+    if (r <= g && r <= b) {
+        if (g <= b) { c0 = r; c1 = g - r; c2 = b - g; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_BLUE; }
+        else { c0 = r; c1 = b - r; c2 = g - b; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_GREEN; }
+    } else if (g <= r && g < b) {
+        if (r <= b) { c0 = g; c1 = r - g; c2 = b - r; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_BLUE; }
+        else { c0 = g; c1 = b - g; c2 = r - b; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_RED; }
+    } else {
+        if (r <= g) { c0 = b; c1 = r - b; c2 = g - r; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_GREEN; }
+        else { c0 = b; c1 = g - b; c2 = r - g; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_RED; }
+    }
+    for (int i = 0; i < 32; ++i)
+        out[i] = c0 * vr_rgbspec_basis[VR_RGBSPEC_WHITE][i] + c1 * vr_rgbspec_basis[kx][i] +
+                 c2 * vr_rgbspec_basis[ky][i];
+    return VR_OK;
+}
+
+double vr_spectrum_intensity_at_wavelength(const vr_spectrum* sp, double wl) {
+    if (!sp || sp->sample_count < 1) return 0.0;
+    if (wl < sp->shortest_wavelength || wl > sp->longest_wavelength) return 0.0;
+    const int n = (int)sp->sample_count;
+    const double range = sp->longest_wavelength - sp->shortest_wavelength;
+    const size_t i = (size_t)((double)(n - 1) * ((wl - sp->shortest_wavelength) / range));
+    const double before = (double)i / (double)(n - 1) * range + sp->shortest_wavelength;
+    if (i == (size_t)(n - 1)) return sp->samples[i];
+    const double after = (double)(i + 1) / (double)(n - 1) * range + sp->shortest_wavelength;
+    const double delta = after - before;
+    const double ratio = (wl - before) / delta;
+    return sp->samples[i] * (1.0 - ratio) + sp->samples[i + 1] * ratio;
+}
+
+static double gaussian_h(double wl, double alpha, double mu, double s1, double s2) {
+    double s = wl < mu ? s1 : s2;
+    double denominator = 2.0 * (s * s);
+    double t = wl - mu;
+    return alpha * std::exp(-(t * t) / denominator);
+}
+
+void vr_colour_xyz_for_wavelength(double wl, double out[3]) {
+    out[0] = gaussian_h(wl, 1.056, 599.8, 37.9, 31.0) + gaussian_h(wl, 0.362, 442.0, 16.0, 26.7) +
+             gaussian_h(wl, -0.065, 501.1, 20.4, 26.2);
+    out[1] = gaussian_h(wl, 0.821, 568.8, 46.9, 40.5) + gaussian_h(wl, 0.286, 530.9, 16.3, 31.1);
+    out[2] = gaussian_h(wl, 1.217, 437.0, 11.8, 36.0) + gaussian_h(wl, 0.681, 459.0, 26.0, 13.8);
+}
+
+int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, vr_scene** out) {
+    if (!desc || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null desc or out");
+    *out = nullptr;
+    vr_scene* s = new (std::nothrow) vr_scene();
+    if (!s) return fail(VR_ERROR_OUT_OF_MEMORY, "scene allocation failed");
+    s->device = device;
+    s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
+    s->camera[0] = desc->camera_location.x;
+    s->camera[1] = desc->camera_location.y;
+    s->camera[2] = desc->camera_location.z;
+    double extent = std::max({std::fabs(s->camera[0]), std::fabs(s->camera[1]), std::fabs(s->camera[2])});
+    auto bad = [&](const std::string& m) {
+        delete s;
+        return fail(VR_ERROR_INVALID_ARGUMENT, m);
+    };
+
+    for (uint32_t i = 0; i < desc->material_count; ++i) {
+        const vr_material_desc& m = desc->materials[i];
+        if (m.kind != VR_MATERIAL_LAMBERTIAN && m.kind != VR_MATERIAL_REFLECTIVE) return bad("unknown material kind");
+        if (m.colour.sample_count < 1 || m.colour.sample_count > VR_MAX_SPECTRUM_SAMPLES || !m.colour.samples)
+            return bad("material spectrum needs 1..64 samples");
+        vr::Material dm{};
+        dm.kind = m.kind;
+        dm.n = (int32_t)m.colour.sample_count;
+        dm.shortest = m.colour.shortest_wavelength;
+        dm.longest = m.colour.longest_wavelength;
+        dm.diffuse = m.diffuse_strength;
+        dm.reflection = m.reflection_strength;
+        std::memcpy(dm.samples, m.colour.samples, sizeof(double) * m.colour.sample_count);
+        s->materials.push_back(dm);
+    }
+    // objects: primitive lists keep their order; BVHs are built per mesh
+    std::vector<int> mesh_object(desc->mesh_count, -1);
+    for (uint32_t oi = 0; oi < desc->object_count; ++oi) {
+        const vr_object_desc& o = desc->objects[oi];
+        if (o.kind == VR_OBJECT_PRIMITIVE_LIST) {
+            if ((uint64_t)o.first + o.count > desc->primitive_count) return bad("primitive list out of range");
+            for (uint32_t k = 0; k < o.count; ++k) {
+                const vr_primitive_desc& p = desc->primitives[o.first + k];
+                if (p.material >= desc->material_count) return bad("primitive material out of range");
+                vr::Prim dp{};
+                dp.kind = p.kind;
+                dp.material = (int32_t)p.material;
+                dp.object = (int32_t)oi;
+                dp.position = (int32_t)k;
+                dp.scalar = p.scalar;
+                if (p.kind == VR_PRIMITIVE_PLANE) {
+                    // Plane::new (plane.rs:18-31)
+                    H3 n = hnormalize({p.vector.x, p.vector.y, p.vector.z});
+                    double ax = std::fabs(n.x), ay = std::fabs(n.y), az = std::fabs(n.z);
+                    int k2 = ax < ay ? (ax < az ? 0 : 2) : (ay < az ? 1 : 2);  // smallest_coord
+                    H3 axis{k2 == 0 ? 1.0 : 0.0, k2 == 1 ? 1.0 : 0.0, k2 == 2 ? 1.0 : 0.0};
+                    H3 cot = hnormalize(hcross(n, axis));
+                    H3 tan = hcross(n, cot);
+                    dp.vec[0] = n.x; dp.vec[1] = n.y; dp.vec[2] = n.z;
+                    dp.tan[0] = tan.x; dp.tan[1] = tan.y; dp.tan[2] = tan.z;
+                    dp.cot[0] = cot.x; dp.cot[1] = cot.y; dp.cot[2] = cot.z;
+                    extent = std::max(extent, std::fabs(p.scalar));
+                } else if (p.kind == VR_PRIMITIVE_SPHERE) {
+                    dp.vec[0] = p.vector.x; dp.vec[1] = p.vector.y; dp.vec[2] = p.vector.z;
+                    extent = std::max({extent, std::fabs(p.vector.x) + std::fabs(p.scalar),
+                                       std::fabs(p.vector.y) + std::fabs(p.scalar),
+                                       std::fabs(p.vector.z) + std::fabs(p.scalar)});
+                } else {
+                    return bad("unknown primitive kind");
+                }
+                s->prims.push_back(dp);
+            }
+        } else if (o.kind == VR_OBJECT_BVH) {
+            if (o.first >= desc->mesh_count) return bad("BVH object mesh out of range");
+            if (mesh_object[o.first] >= 0) return bad("a mesh can back only one BVH object");
+            mesh_object[o.first] = (int)oi;
+        } else {
+            return bad("unknown object kind");
+        }
+    }
+    s->object_count = desc->object_count;
+    s->leaf_order.resize(desc->mesh_count);
+    s->mesh_tri_base.assign(desc->mesh_count, 0);
+    for (uint32_t mi = 0; mi < desc->mesh_count; ++mi) {
+        const vr_mesh_desc& m = desc->meshes[mi];
+        if (m.triangle_count && (!m.vertices || !m.normals)) return bad("mesh without vertex or normal arrays");
+        if (m.material >= desc->material_count) return bad("mesh material out of range");
+        if (s->tris.size() + m.triangle_count > (uint64_t)INT32_MAX) return bad("too many triangles (2^31)");
+        BvhBuilder B;
+        B.tri_base = (int)s->tris.size();
+        s->mesh_tri_base[mi] = B.tri_base;
+        B.prims.resize(m.triangle_count);
+        for (uint64_t t = 0; t < m.triangle_count; ++t) {
+            Box3 bb = box_empty();  // BoundingBox::from_points(&vertices) (triangle.rs:101-105)
+            for (int k = 0; k < 3; ++k)
+                for (int c = 0; c < 3; ++c) {
+                    double v = m.vertices[9 * t + 3 * k + c];
+                    bb.b[c] = iv_expand(bb.b[c], v);
+                    extent = std::max(extent, std::fabs(v));
+                }
+            B.prims[t].box = bb;
+            for (int c = 0; c < 3; ++c) B.prims[t].centre[c] = (bb.b[c].min + bb.b[c].max) / 2.0;  // centre()
+            B.prims[t].orig = t;
+        }
+        vr::Bvh bvh{};
+        bvh.object = mesh_object[mi];
+        bvh.tri_base = B.tri_base;
+        bvh.material = (int32_t)m.material;
+        if (m.triangle_count == 0) {
+            bvh.root = INT32_MIN;
+            for (int i = 0; i < 6; ++i) bvh.root_box[i] = (i & 1) ? -INFINITY : INFINITY;
+        } else {
+            Box3 rb;
+            B.nodes.reserve(m.triangle_count);
+            int32_t root = B.build(0, m.triangle_count, 0, rb);
+            box_to_layout(rb, bvh.root_box);
+            // re-base interior node indices into the scene-wide node array
+            const int32_t node_base = (int32_t)s->nodes.size();
+            for (auto& n : B.nodes)
+                for (int c = 0; c < 2; ++c)
+                    if (n.child[c] >= 0) n.child[c] += node_base;
+            bvh.root = root >= 0 ? root + node_base : root;
+            s->nodes.insert(s->nodes.end(), B.nodes.begin(), B.nodes.end());
+            s->max_depth = std::max(s->max_depth, B.max_depth);
+        }
+        s->leaf_order[mi].resize(m.triangle_count);
+        for (uint64_t i = 0; i < m.triangle_count; ++i) {
+            const uint64_t t = B.prims[i].orig;
+            s->leaf_order[mi][i] = t;
+            vr::TriVerts tv{};
+            vr::TriNormals tn{};
+            std::memcpy(tv.v, m.vertices + 9 * t, 9 * sizeof(double));
+            std::memcpy(tn.n, m.normals + 9 * t, 9 * sizeof(double));
+            s->tris.push_back(tv);
+            s->normals.push_back(tn);
+        }
+        if (mesh_object[mi] >= 0) s->bvhs.push_back(bvh);
+    }
+    // BVH objects in object order (ties across objects depend on it)
+    std::sort(s->bvhs.begin(), s->bvhs.end(), [](const vr::Bvh& a, const vr::Bvh& b) { return a.object < b.object; });
+    s->extent = extent;
+    vr::DeviceScene& d = s->dev;
+    d.prim_count = (int32_t)s->prims.size();
+    d.bvh_count = (int32_t)s->bvhs.size();
+    std::memcpy(d.camera, s->camera, sizeof d.camera);
+    d.margin = 1e-9 * (extent + 1.0);
+    d.behind_margin = 1e-6 * (extent + 1.0);
+    if (!s->host_only) {
+        int rc = upload(s);
+        if (rc != VR_OK) {
+            std::string msg = g_last_error;
+            vr_scene_destroy(s);
+            return fail(rc, msg);
+        }
+    }
+    *out = s;
+    return VR_OK;
+}
+
+void vr_scene_destroy(vr_scene* s) {
+    if (!s) return;
+    if (s->d_block) {
+        (void)hipSetDevice(s->device);
+        (void)hipFree(s->d_block);
+    }
+    delete s;
+}
+
+int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
+    if (!s || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    out->triangle_count = s->tris.size();
+    out->node_count = s->nodes.size();
+    out->max_bvh_depth = (uint32_t)s->max_depth;
+    out->object_count = s->object_count;
+    out->extent = s->extent;
+    out->device_bytes = s->device_bytes;
+    return VR_OK;
+}
+
+int vr_scene_bvh_leaf_order(const vr_scene* s, uint32_t mesh, uint64_t* out) {
+    if (!s || !out || mesh >= s->leaf_order.size()) return fail(VR_ERROR_INVALID_ARGUMENT, "bad mesh index");
+    std::memcpy(out, s->leaf_order[mesh].data(), sizeof(uint64_t) * s->leaf_order[mesh].size());
+    return VR_OK;
+}
+
+int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* state, void* stream,
+                          uint32_t launch_flags, vr_launch_stats* stats) {
+    int rc = check_render_params(s, p);
+    if (rc) return rc;
+    if (!state) return fail(VR_ERROR_INVALID_ARGUMENT, "null state");
+    VR_HIP(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    vr_scene* ms = const_cast<vr_scene*>(s);
+    vr::RenderArgs a = make_args(s, p, state);
+    const bool counting = (launch_flags & VR_LAUNCH_COUNTERS) != 0;
+    const bool timed = (launch_flags & VR_LAUNCH_TIMED) != 0 || counting;
+    std::unique_lock<std::mutex> lock(ms->counter_mutex, std::defer_lock);
+    if (counting) {
+        lock.lock();
+        VR_HIP(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long) * vr::kCntCount, st));
+        a.counters = s->d_counters;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timed) {
+        VR_HIP(hipEventCreate(&e0));
+        VR_HIP(hipEventCreate(&e1));
+        VR_HIP(hipEventRecord(e0, st));
+    }
+    int lr = vr::launch_render(a, stack_depth(s), counting, false, st);
+    if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    if (timed) {
+        VR_HIP(hipEventRecord(e1, st));
+        VR_HIP(hipEventSynchronize(e1));
+        float ms_ = 0.f;
+        VR_HIP(hipEventElapsedTime(&ms_, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (stats) {
+            std::memset(stats, 0, sizeof *stats);
+            stats->kernel_ms = ms_;
+            stats->timed = 1;
+        }
+        if (counting) {
+            unsigned long long c[vr::kCntCount];
+            VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+            if (stats) {
+                stats->box_tests = c[vr::kCntBoxTests];
+                stats->node_visits = c[vr::kCntNodeVisits];
+                stats->triangle_tests = c[vr::kCntTriangleTests];
+                stats->rays = c[vr::kCntRays];
+                stats->shaded_triangle_hits = c[vr::kCntShadedTriangles];
+                stats->samples = c[vr::kCntSamples];
+            }
+        }
+        return read_and_clear_error(s, st);
+    }
+    return VR_OK;
+}
+
+int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation_buffer* buf) {
+    int rc = check_render_params(s, p);
+    if (rc) return rc;
+    const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
+    if (!buf || buf->width != tw || buf->height != th || !buf->colour || !buf->colour_sum || !buf->colour_bias ||
+        !buf->weight || !buf->weight_bias)
+        return fail(VR_ERROR_INVALID_ARGUMENT, "accumulation buffer does not match the tile");
+    const uint64_t n = tw * th;
+    if (n == 0) return VR_OK;
+    VR_HIP(hipSetDevice(s->device));
+    CallScratch cs;
+    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    std::vector<double> host(n * 8, 0.0);
+    if (p->accumulate) {
+        for (uint64_t i = 0; i < n; ++i) {
+            for (int k = 0; k < 3; ++k) {
+                host[8 * i + k] = buf->colour_sum[3 * i + k];
+                host[8 * i + 3 + k] = buf->colour_bias[3 * i + k];
+            }
+            host[8 * i + 6] = buf->weight[i];
+            host[8 * i + 7] = buf->weight_bias[i];
+        }
+    }
+    VR_HIP(hipMalloc(&cs.ptr, n * 8 * sizeof(double)));
+    VR_HIP(hipMemcpyAsync(cs.ptr, host.data(), n * 8 * sizeof(double), hipMemcpyHostToDevice, cs.stream));
+    rc = vr_render_tile_device(s, p, (double*)cs.ptr, cs.stream, 0, nullptr);
+    if (rc) return rc;
+    VR_HIP(hipMemcpyAsync(host.data(), cs.ptr, n * 8 * sizeof(double), hipMemcpyDeviceToHost, cs.stream));
+    VR_HIP(hipStreamSynchronize(cs.stream));
+    rc = read_and_clear_error(s, cs.stream);
+    for (uint64_t i = 0; i < n; ++i) {
+        const double w = host[8 * i + 6];
+        const double inv = 1.0 / w;  // accumulation_buffer.rs:59
+        for (int k = 0; k < 3; ++k) {
+            buf->colour_sum[3 * i + k] = host[8 * i + k];
+            buf->colour_bias[3 * i + k] = host[8 * i + 3 + k];
+            buf->colour[3 * i + k] = w != 0.0 ? host[8 * i + k] * inv : 0.0;
+        }
+        buf->weight[i] = w;
+        buf->weight_bias[i] = host[8 * i + 7];
+    }
+    return rc;
+}
+
+int vr_partial_render_scene(const vr_scene* s, vr_tile tile, uint64_t height, uint64_t width,
+                            vr_accumulation_buffer* out) {
+    if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
+    vr_render_params p{};
+    p.tile = tile;
+    p.height = height;
+    p.width = width;
+    p.spp = 1;
+    p.accumulate = 0;
+    p.seed = s->partial_seed;
+    p.first_sample = const_cast<vr_scene*>(s)->pass_counter.fetch_add(1);
+    return vr_render_tile(s, &p, out);
+}
+
+int vr_render_samples(const vr_scene* s, const vr_render_params* p, vr_sample_record* out) {
+    int rc = check_render_params(s, p);
+    if (rc) return rc;
+    if (!out) return fail(VR_ERROR_INVALID_ARGUMENT, "null output");
+    const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
+    const uint64_t n = tw * th;
+    if (n == 0 || p->spp == 0) return VR_OK;
+    VR_HIP(hipSetDevice(s->device));
+    CallScratch cs, rec;
+    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    VR_HIP(hipMalloc(&cs.ptr, n * 8 * sizeof(double)));
+    VR_HIP(hipMemsetAsync(cs.ptr, 0, n * 8 * sizeof(double), cs.stream));
+    const size_t rec_bytes = n * p->spp * sizeof(vr_sample_record);
+    VR_HIP(hipMalloc(&rec.ptr, rec_bytes));
+    vr_render_params q = *p;
+    q.accumulate = 0;
+    vr::RenderArgs a = make_args(s, &q, (double*)cs.ptr);
+    a.records = rec.ptr;
+    int lr = vr::launch_render(a, stack_depth(s), false, true, cs.stream);
+    if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    VR_HIP(hipMemcpyAsync(out, rec.ptr, rec_bytes, hipMemcpyDeviceToHost, cs.stream));
+    VR_HIP(hipStreamSynchronize(cs.stream));
+    return read_and_clear_error(s, cs.stream);
+}
+
+int vr_trace_rays(const vr_scene* s, uint64_t n, const double* origins, const double* directions,
+                  vr_hit_record* out) {
+    if (!s || (n && (!origins || !directions || !out))) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
+    if (n == 0) return VR_OK;
+    VR_HIP(hipSetDevice(s->device));
+    CallScratch cs;
+    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    const size_t in_bytes = n * 3 * sizeof(double), out_bytes = n * sizeof(vr_hit_record);
+    VR_HIP(hipMalloc(&cs.ptr, 2 * in_bytes + out_bytes));
+    char* b = (char*)cs.ptr;
+    VR_HIP(hipMemcpyAsync(b, origins, in_bytes, hipMemcpyHostToDevice, cs.stream));
+    VR_HIP(hipMemcpyAsync(b + in_bytes, directions, in_bytes, hipMemcpyHostToDevice, cs.stream));
+    VR_HIP(hipMemsetAsync(b + 2 * in_bytes, 0, out_bytes, cs.stream));
+    vr::TraceArgs a{};
+    a.scene = s->dev;
+    a.n = n;
+    a.origins = (const double*)b;
+    a.directions = (const double*)(b + in_bytes);
+    a.out = b + 2 * in_bytes;
+    int lr = vr::launch_trace(a, stack_depth(s), cs.stream);
+    if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    VR_HIP(hipMemcpyAsync(out, b + 2 * in_bytes, out_bytes, hipMemcpyDeviceToHost, cs.stream));
+    VR_HIP(hipStreamSynchronize(cs.stream));
+    return VR_OK;
+}
+
+int vr_resolve_state(const double* state, uint64_t pixel_count, double* colour) {
+    if (!state || !colour) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    for (uint64_t i = 0; i < pixel_count; ++i) {
+        const double w = state[8 * i + 6];
+        const double inv = 1.0 / w;
+        for (int k = 0; k < 3; ++k) colour[3 * i + k] = w != 0.0 ? state[8 * i + k] * inv : 0.0;
+    }
+    return VR_OK;
+}
+
+// mesh::load_obj (src/mesh.rs:13-88) over the obj 0.9 crate's parsing: "v x y z" and
+// "vn x y z" as f32 (correctly rounded strtof) widened to f64, "f a b c ..." with a, a/t,
+// a//n or a/t/n corners (1-based, negative = relative), fan triangles (v0, v_i, v_{i+1}).
+int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, double** normals) {
+    if (!path || !triangle_count || !vertices || !normals) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(VR_ERROR_IO, std::string("cannot open ") + path);
+    std::vector<float> pos, nrm;
+    struct Corner {
+        int64_t v, n;
+    };
+    std::vector<double> vout, nout;
+    std::vector<Corner> poly;
+    char line[4096];
+    int64_t lineno = 0;
+    auto resolve = [](int64_t idx, size_t count) -> int64_t {
+        if (idx > 0) return idx - 1;
+        if (idx < 0) return (int64_t)count + idx;
+        return -1;
+    };
+    int status = VR_OK;
+    std::string err;
+    while (std::fgets(line, sizeof line, f)) {
+        ++lineno;
+        char* s = line;
+        while (*s == ' ' || *s == '\t') ++s;
+        if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) {
+            char* e = s + 1;
+            for (int k = 0; k < 3; ++k) pos.push_back(std::strtof(e, &e));
+        } else if (s[0] == 'v' && s[1] == 'n' && (s[2] == ' ' || s[2] == '\t')) {
+            char* e = s + 2;
+            for (int k = 0; k < 3; ++k) nrm.push_back(std::strtof(e, &e));
+        } else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
+            poly.clear();
+            char* e = s + 1;
+            while (true) {
+                while (*e == ' ' || *e == '\t') ++e;
+                if (*e == '\0' || *e == '\n' || *e == '\r' || *e == '#') break;
+                char* q;
+                long long vi = std::strtoll(e, &q, 10);
+                if (q == e) {
+                    status = VR_ERROR_IO;
+                    err = "malformed face at line " + std::to_string(lineno);
+                    break;
+                }
+                e = q;
+                long long ni = 0;
+                if (*e == '/') {
+                    ++e;
+                    if (*e != '/') std::strtoll(e, &e, 10);  // texture index: unused (mesh.rs:19)
+                    if (*e == '/') {
+                        ++e;
+                        ni = std::strtoll(e, &e, 10);
+                    }
+                }
+                Corner c{resolve(vi, pos.size() / 3), ni ? resolve(ni, nrm.size() / 3) : -1};
+                if (c.v < 0 || (size_t)c.v >= pos.size() / 3 || (ni && (c.n < 0 || (size_t)c.n >= nrm.size() / 3))) {
+                    status = VR_ERROR_IO;
+                    err = "face index out of range at line " + std::to_string(lineno);
+                    break;
+                }
+                poly.push_back(c);
+                while (*e && *e != ' ' && *e != '\t' && *e != '\n' && *e != '\r') ++e;
+            }
+            if (status != VR_OK) break;
+            for (size_t i = 1; i + 1 < poly.size(); ++i) {
+                const Corner cs3[3] = {poly[0], poly[i], poly[i + 1]};
+                for (const Corner& c : cs3) {
+                    for (int k = 0; k < 3; ++k) vout.push_back((double)pos[3 * c.v + k]);
+                    for (int k = 0; k < 3; ++k) nout.push_back(c.n >= 0 ? (double)nrm[3 * c.n + k] : 0.0);
+                }
+            }
+        }
+    }
+    std::fclose(f);
+    if (status != VR_OK) return fail(status, err);
+    const uint64_t n = vout.size() / 9;
+    double* v = (double*)std::malloc(sizeof(double) * std::max<size_t>(vout.size(), 1));
+    double* nn = (double*)std::malloc(sizeof(double) * std::max<size_t>(nout.size(), 1));
+    if (!v || !nn) {
+        std::free(v);
+        std::free(nn);
+        return fail(VR_ERROR_OUT_OF_MEMORY, "mesh allocation failed");
+    }
+    std::memcpy(v, vout.data(), sizeof(double) * vout.size());
+    std::memcpy(nn, nout.data(), sizeof(double) * nout.size());
+    *triangle_count = n;
+    *vertices = v;
+    *normals = nn;
+    return VR_OK;
+}
+
+void vr_mesh_free(double* vertices, double* normals) {
+    std::free(vertices);
+    std::free(normals);
+}
+
+}  // extern "C"

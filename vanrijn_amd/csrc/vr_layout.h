@@ -1,0 +1,122 @@
+// vr_layout.h -- HBM layout of a flattened scene and the kernel parameter blocks.
+//
+// Shared by the host side (vr_scene.cpp, vr_capi.cpp) and the gfx950 kernels (vr_render.hip).
+// Sizes are chosen for 64-lane waves doing independent per-lane gathers: every record a lane
+// reads whole is a multiple of 16 B and 16-B aligned so it is fetched with dwordx4 loads.
+#pragma once
+
+#include <stdint.h>
+
+namespace vr {
+
+constexpr int kRecursionLimit = 128;       // camera.rs:69
+constexpr int kMaxSpectrumSamples = 64;
+constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
+
+// One interior node of a binary BVH, child boxes stored in the parent so a visit tests both
+// children with one 128-B record.  box[c] = {min x, max x, min y, max y, min z, max z} of child c
+// (its own bounds in the reference tree, bounding_volume_hierarchy.rs:18-28).  child[c] >= 0:
+// interior node index; child[c] < 0: leaf holding triangle ~child[c] (leaf size is always 1,
+// bounding_volume_hierarchy.rs:57).
+struct alignas(128) Node {
+    double box[2][6];  // 96 B
+    int32_t child[2];  //  8 B
+    int32_t pad[6];    // 24 B -> 128 B, one cache line
+};
+static_assert(sizeof(Node) == 128, "Node must be one 128-B line");
+
+// Triangle vertices in BVH leaf order, padded to 80 B for 16-B aligned loads.
+struct alignas(16) TriVerts {
+    double v[9];
+    double pad;
+};
+static_assert(sizeof(TriVerts) == 80, "TriVerts must be 80 B");
+
+// Shading normals, same order (read once per closest triangle hit).
+struct alignas(16) TriNormals {
+    double n[9];
+    double pad;
+};
+
+struct Material {
+    int32_t kind;  // 0 Lambertian, 1 Reflective
+    int32_t n;     // spectrum sample count
+    double shortest, longest;
+    double diffuse, reflection;
+    double pad;
+    double samples[kMaxSpectrumSamples];
+};
+
+// Plane (after Plane::new) or sphere.
+struct Prim {
+    int32_t kind;      // 0 plane, 1 sphere
+    int32_t material;
+    int32_t object;    // scene object index
+    int32_t position;  // position inside its primitive list
+    double vec[3];     // plane normal / sphere centre
+    double tan[3];     // plane tangent
+    double cot[3];     // plane cotangent
+    double scalar;     // plane distance / sphere radius
+};
+
+struct Bvh {
+    double root_box[6];  // bounds of the whole tree (tested first, as the reference's root)
+    int32_t root;        // >= 0 interior node, < 0 leaf ~triangle, INT32_MIN: empty mesh
+    int32_t object;      // scene object index
+    int32_t tri_base;    // first triangle of this mesh in the global leaf-ordered arrays
+    int32_t material;
+};
+
+// Device view of a scene (all pointers are device pointers on one GPU).
+struct DeviceScene {
+    const Node* nodes;
+    const TriVerts* tris;
+    const TriNormals* normals;
+    const Material* materials;
+    const Prim* prims;
+    const Bvh* bvhs;
+    int32_t prim_count;
+    int32_t bvh_count;
+    double camera[3];
+    double margin;         // distance-cull slack (absolute + relative), see DESIGN.md "Traversal"
+    double behind_margin;  // cull of boxes entirely behind the origin
+};
+
+struct RenderArgs {
+    DeviceScene scene;
+    uint64_t start_column, start_row, tile_width, tile_height;
+    uint64_t width, height;
+    uint64_t seed, first_sample;
+    uint32_t spp;
+    uint32_t accumulate;
+    double* state;             // [tile pixels][8]
+    void* records;             // vr_sample_record* (record variant) or nullptr
+    unsigned long long* counters;  // [8] (counting variant) or nullptr
+    int32_t* error_flag;
+};
+
+struct TraceArgs {
+    DeviceScene scene;
+    uint64_t n;
+    const double* origins;
+    const double* directions;
+    void* out;  // vr_hit_record*
+};
+
+// counters[] slots of the counting kernel variant
+enum Counter : int {
+    kCntBoxTests = 0,
+    kCntNodeVisits = 1,
+    kCntTriangleTests = 2,
+    kCntRays = 3,
+    kCntShadedTriangles = 4,
+    kCntSamples = 5,
+    kCntCount = 8
+};
+
+// Launch wrappers implemented in vr_render.hip (host-callable).
+int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, void* stream);
+int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
+const char* device_error_string(int code);
+
+}  // namespace vr

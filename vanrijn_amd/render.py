@@ -1,0 +1,189 @@
+"""Render API mirroring the reference (camera.rs, accumulation_buffer.rs, util/tile_iterator.rs).
+
+    partial_render_scene(scene, tile, height, width) -> AccumulationBuffer   camera.rs:95-130
+    AccumulationBuffer::{new, update_pixel, merge_tile}                     accumulation_buffer.rs:14-85
+    Tile / TileIterator                                                     util/tile_iterator.rs:1-67
+
+Every render call goes through the C ABI into the gfx950 kernels; nothing here computes a pixel.
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+RECURSION_LIMIT = 128  # camera.rs:69
+SAMPLE_RECORD_DTYPE = np.dtype([("wavelength", "<f8"), ("intensity", "<f8"), ("xyz", "<f8", (3,)),
+                                ("bounces", "<i4"), ("flags", "<i4")])
+HIT_RECORD_DTYPE = np.dtype([("valid", "<i4"), ("object", "<i4"), ("primitive", "<i8"), ("distance", "<f8"),
+                             ("location", "<f8", (3,)), ("normal", "<f8", (3,)), ("tangent", "<f8", (3,)),
+                             ("cotangent", "<f8", (3,)), ("retro", "<f8", (3,))])
+assert SAMPLE_RECORD_DTYPE.itemsize == C.sizeof(N.SampleRecord)
+assert HIT_RECORD_DTYPE.itemsize == C.sizeof(N.HitRecord)
+
+
+@dataclass(frozen=True)
+class Tile:
+    start_column: int
+    end_column: int
+    start_row: int
+    end_row: int
+
+    def width(self):
+        return self.end_column - self.start_column
+
+    def height(self):
+        return self.end_row - self.start_row
+
+    def _c(self):
+        return N.TileC(self.start_column, self.end_column, self.start_row, self.end_row)
+
+
+class TileIterator:
+    """Row-major tiles of at most tile_size x tile_size covering the image exactly once."""
+
+    def __init__(self, total_width, total_height, tile_size):
+        assert tile_size > 0
+        self.w, self.h, self.s = total_width, total_height, tile_size
+
+    def __iter__(self):
+        row = 0
+        while row < self.h:
+            col = 0
+            while col < self.w:
+                yield Tile(col, min(self.w, col + self.s), row, min(self.h, row + self.s))
+                col += self.s
+            row += self.s
+
+
+class AccumulationBuffer:
+    """Per-pixel Kahan-compensated XYZ sums and weights; `colour` is the running mean.
+
+    Arrays are [height][width][3] (XYZ) and [height][width] (weights), row-major like Array2D.
+    The reference's `new(a, b)` names its parameters (height, width) but yields width = a,
+    height = b (accumulation_buffer.rs:15-28 via array2d.rs:13-19); `new(width, height)` here.
+    """
+
+    def __init__(self, width, height):
+        self.colour_buffer = np.zeros((height, width, 3))
+        self.colour_sum_buffer = np.zeros((height, width, 3))
+        self.colour_bias_buffer = np.zeros((height, width, 3))
+        self.weight_buffer = np.zeros((height, width))
+        self.weight_bias_buffer = np.zeros((height, width))
+
+    @staticmethod
+    def new(width, height):
+        return AccumulationBuffer(width, height)
+
+    def width(self):
+        return self.colour_buffer.shape[1]
+
+    def height(self):
+        return self.colour_buffer.shape[0]
+
+    def _c(self):
+        for a in (self.colour_buffer, self.colour_sum_buffer, self.colour_bias_buffer, self.weight_buffer,
+                  self.weight_bias_buffer):
+            assert a.flags.c_contiguous and a.dtype == np.float64
+        return N.AccumulationBufferC(self.width(), self.height(), self.colour_buffer.ctypes.data,
+                                     self.colour_sum_buffer.ctypes.data, self.colour_bias_buffer.ctypes.data,
+                                     self.weight_buffer.ctypes.data, self.weight_bias_buffer.ctypes.data)
+
+    def merge_tile(self, tile: Tile, src: "AccumulationBuffer"):
+        """accumulation_buffer.rs:62-85: weighted blend of the means; weights add."""
+        assert tile.width() == src.width() and tile.height() == src.height()
+        dc = self.colour_buffer[tile.start_row:tile.end_row, tile.start_column:tile.end_column]
+        dw = self.weight_buffer[tile.start_row:tile.end_row, tile.start_column:tile.end_column]
+        w1, w2 = dw[..., None], src.weight_buffer[..., None]
+        dc[...] = (dc * w1 + src.colour_buffer * w2) * (1.0 / (w1 + w2))
+        dw += src.weight_buffer
+
+    @staticmethod
+    def from_state(state):
+        """Build from device-state records [h][w][8] = {sum XYZ, bias XYZ, weight, weight_bias}."""
+        s = np.asarray(state, dtype=np.float64)
+        h, w = s.shape[:2]
+        b = AccumulationBuffer(w, h)
+        b.colour_sum_buffer[...] = s[..., 0:3]
+        b.colour_bias_buffer[...] = s[..., 3:6]
+        b.weight_buffer[...] = s[..., 6]
+        b.weight_bias_buffer[...] = s[..., 7]
+        wgt = s[..., 6:7]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            b.colour_buffer[...] = np.where(wgt != 0.0, s[..., 0:3] * (1.0 / wgt), 0.0)
+        return b
+
+
+def _scene_handle(scene, device):
+    from .scene import DeviceScene, Scene
+    if isinstance(scene, DeviceScene):
+        return scene
+    if isinstance(scene, Scene):
+        return scene.device_scene(device)
+    raise TypeError("expected Scene or DeviceScene")
+
+
+def _params(tile, height, width, spp, seed, first_sample, accumulate):
+    return N.RenderParams(tile._c(), height, width, spp, 1 if accumulate else 0, seed, first_sample)
+
+
+def partial_render_scene(scene, tile: Tile, height: int, width: int, device=0) -> AccumulationBuffer:
+    """camera.rs:95-130: one sample per pixel of `tile` into a fresh tile AccumulationBuffer."""
+    ds = _scene_handle(scene, device)
+    out = AccumulationBuffer(tile.width(), tile.height())
+    oc = out._c()
+    N.check(N.lib().vr_partial_render_scene(ds.handle, tile._c(), height, width, C.byref(oc)))
+    return out
+
+
+def render_tile(scene, tile: Tile, height, width, spp, seed, first_sample=0, accumulate: AccumulationBuffer = None,
+                device=0) -> AccumulationBuffer:
+    """spp samples per pixel with explicit seed / sample range (update_pixel semantics)."""
+    ds = _scene_handle(scene, device)
+    buf = accumulate if accumulate is not None else AccumulationBuffer(tile.width(), tile.height())
+    bc = buf._c()
+    p = _params(tile, height, width, spp, seed, first_sample, accumulate is not None)
+    N.check(N.lib().vr_render_tile(ds.handle, C.byref(p), C.byref(bc)))
+    return buf
+
+
+def render_samples(scene, tile: Tile, height, width, spp, seed, first_sample=0, device=0):
+    """Per-(pixel, sample) records [tile_h][tile_w][spp] (decision-identity checks)."""
+    ds = _scene_handle(scene, device)
+    out = np.zeros(tile.width() * tile.height() * spp, dtype=SAMPLE_RECORD_DTYPE)
+    p = _params(tile, height, width, spp, seed, first_sample, False)
+    N.check(N.lib().vr_render_samples(ds.handle, C.byref(p), out.ctypes.data_as(C.c_void_p)))
+    return out.reshape(tile.height(), tile.width(), spp)
+
+
+def trace_rays(scene, origins, directions, device=0):
+    """Sampler::sample for a batch of rays (directions used as given)."""
+    ds = _scene_handle(scene, device)
+    o = np.ascontiguousarray(origins, dtype=np.float64).reshape(-1, 3)
+    d = np.ascontiguousarray(directions, dtype=np.float64).reshape(-1, 3)
+    out = np.zeros(len(o), dtype=HIT_RECORD_DTYPE)
+    N.check(N.lib().vr_trace_rays(ds.handle, len(o), o.ctypes.data_as(C.c_void_p), d.ctypes.data_as(C.c_void_p),
+                                  out.ctypes.data_as(C.c_void_p)))
+    return out
+
+
+def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample, state_ptr, stream_ptr=None,
+                       accumulate=False, timed=False, counters=False, device=0):
+    """Enqueue a render into device state records (8 f64 per pixel) at `state_ptr` (a device
+    pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel time when timed)."""
+    ds = _scene_handle(scene, device)
+    p = _params(tile, height, width, spp, seed, first_sample, accumulate)
+    st = N.LaunchStats()
+    flags = (N.LAUNCH_TIMED if timed else 0) | (N.LAUNCH_COUNTERS if counters else 0)
+    N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
+                                          C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
+    return st.as_dict()
+
+
+def resolve_state(state):
+    """Mean XYZ [.., 3] of state records [.., 8] (accumulation_buffer.rs:59)."""
+    s = np.ascontiguousarray(state, dtype=np.float64)
+    out = np.zeros(s.shape[:-1] + (3,))
+    N.check(N.lib().vr_resolve_state(s.ctypes.data_as(C.c_void_p), s.size // 8, out.ctypes.data_as(C.c_void_p)))
+    return out

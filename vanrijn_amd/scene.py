@@ -1,0 +1,312 @@
+"""Host-side mirror of the reference's scene API (names and argument meaning as in vanrijn).
+
+    colour::ColourRgbF / NamedColour      src/colour/colour_rgb.rs:5-105
+    colour::Spectrum                      src/colour/spectrum.rs:5-175
+    materials::LambertianMaterial         src/materials/lambertian_material.rs:12-25
+    materials::ReflectiveMaterial         src/materials/reflective_material.rs:8-13
+    raycasting::{Plane, Sphere}           src/raycasting/plane.rs:18-31, sphere.rs:15-23
+    raycasting::BoundingVolumeHierarchy   src/raycasting/bounding_volume_hierarchy.rs:49-51
+    mesh::load_obj                        src/mesh.rs:74-88
+    scene::Scene                          src/scene.rs:5-8
+
+A `Scene` lowers to a plain-data `SceneSpec` (numbers only) which the C ABI consumes
+(`vr_scene_create`) -- and which the test oracle consumes too, so both see identical inputs.
+"""
+from dataclasses import dataclass, field
+import ctypes as C
+from enum import Enum
+from typing import List
+
+import numpy as np
+
+from . import _native as N
+
+SHORTEST_VISIBLE_WAVELENGTH = 380.0  # src/colour/mod.rs:13
+LONGEST_VISIBLE_WAVELENGTH = 740.0   # src/colour/mod.rs:14
+
+
+# ------------------------------------------------------------------------------ colours / spectra
+class NamedColour(Enum):
+    Black = (0.0, 0.0, 0.0)
+    White = (1.0, 1.0, 1.0)
+    Red = (1.0, 0.0, 0.0)
+    Lime = (0.0, 1.0, 0.0)
+    Blue = (0.0, 0.0, 1.0)
+    Yellow = (1.0, 1.0, 0.0)
+    Cyan = (0.0, 1.0, 1.0)
+    Magenta = (1.0, 0.0, 1.0)
+    Gray = (0.5, 0.5, 0.5)
+    Maroon = (0.5, 0.0, 0.0)
+    Olive = (0.5, 0.5, 0.0)
+    Green = (0.0, 0.5, 0.0)
+    Purple = (0.5, 0.0, 0.5)
+    Teal = (0.0, 0.5, 0.5)
+    Navy = (0.0, 0.0, 0.5)
+
+
+@dataclass(frozen=True)
+class ColourRgbF:
+    red: float
+    green: float
+    blue: float
+
+    @staticmethod
+    def new(r, g, b):
+        return ColourRgbF(float(r), float(g), float(b))
+
+    @staticmethod
+    def from_named(name: NamedColour):
+        return ColourRgbF(*name.value)
+
+
+@dataclass
+class Spectrum:
+    shortest_wavelength: float
+    longest_wavelength: float
+    samples: np.ndarray
+
+    @staticmethod
+    def black():
+        return Spectrum(SHORTEST_VISIBLE_WAVELENGTH, LONGEST_VISIBLE_WAVELENGTH, np.zeros(2))
+
+    @staticmethod
+    def grey(brightness):
+        return Spectrum(SHORTEST_VISIBLE_WAVELENGTH, LONGEST_VISIBLE_WAVELENGTH, np.full(2, float(brightness)))
+
+    @staticmethod
+    def reflection_from_linear_rgb(colour: ColourRgbF):
+        out = np.zeros(32)
+        N.check(N.lib().vr_spectrum_reflection_from_linear_rgb(colour.red, colour.green, colour.blue,
+                                                                out.ctypes.data_as(C.c_void_p)))
+        return Spectrum(380.0, 720.0, out)
+
+    def intensity_at_wavelength(self, wavelength):
+        s = np.ascontiguousarray(self.samples, dtype=np.float64)
+        sp = N.Spectrum(self.shortest_wavelength, self.longest_wavelength, s.size,
+                        s.ctypes.data_as(C.POINTER(C.c_double)))
+        return N.lib().vr_spectrum_intensity_at_wavelength(C.byref(sp), float(wavelength))
+
+
+# ------------------------------------------------------------------------------ materials
+@dataclass
+class LambertianMaterial:
+    colour: Spectrum
+    diffuse_strength: float
+
+    @staticmethod
+    def new_dummy():  # lambertian_material.rs:19-24
+        return LambertianMaterial(Spectrum.black(), 1.0)
+
+
+@dataclass
+class ReflectiveMaterial:
+    colour: Spectrum
+    diffuse_strength: float
+    reflection_strength: float
+
+
+# ------------------------------------------------------------------------------ geometry
+@dataclass
+class Plane:
+    normal: tuple
+    distance_from_origin: float
+    material: object
+
+
+@dataclass
+class Sphere:
+    centre: tuple
+    radius: float
+    material: object
+
+
+@dataclass
+class Mesh:
+    """A triangle mesh: vertices/normals float64 [n][3][3] (Vec<Triangle>, triangle.rs:8-13)."""
+    vertices: np.ndarray
+    normals: np.ndarray
+    material: object
+
+    def __len__(self):
+        return len(self.vertices)
+
+
+class BoundingVolumeHierarchy:
+    """BoundingVolumeHierarchy::build over a mesh.  The tree is built (with the reference's median
+    split) by the native library when the scene is created."""
+
+    def __init__(self, mesh: Mesh):
+        self.mesh = mesh
+
+    @staticmethod
+    def build(mesh: Mesh):
+        return BoundingVolumeHierarchy(mesh)
+
+
+def load_obj(path, material):
+    """mesh::load_obj: OBJ positions/normals as f32 widened to f64, fan-triangulated polygons."""
+    L = N.lib()
+    n = C.c_uint64()
+    v = C.POINTER(C.c_double)()
+    nn = C.POINTER(C.c_double)()
+    N.check(L.vr_load_obj(str(path).encode(), C.byref(n), C.byref(v), C.byref(nn)))
+    try:
+        cnt = int(n.value) * 9
+        verts = np.ctypeslib.as_array(v, shape=(max(cnt, 1),))[:cnt].copy().reshape(-1, 3, 3)
+        norms = np.ctypeslib.as_array(nn, shape=(max(cnt, 1),))[:cnt].copy().reshape(-1, 3, 3)
+    finally:
+        L.vr_mesh_free(v, nn)
+    return Mesh(verts, norms, material)
+
+
+# ------------------------------------------------------------------------------ plain-data spec
+@dataclass
+class MaterialSpec:
+    kind: int
+    colour: Spectrum
+    diffuse_strength: float
+    reflection_strength: float = 0.0
+
+
+@dataclass
+class PrimitiveSpec:
+    kind: int
+    material: int
+    vector: tuple
+    scalar: float
+
+
+@dataclass
+class MeshSpec:
+    vertices: np.ndarray
+    normals: np.ndarray
+    material: int
+
+
+@dataclass
+class ObjectSpec:
+    kind: str  # "primitives" | "bvh"
+    primitives: List[PrimitiveSpec] = field(default_factory=list)
+    mesh: int = -1
+
+
+@dataclass
+class SceneSpec:
+    camera_location: tuple
+    materials: List[MaterialSpec]
+    meshes: List[MeshSpec]
+    objects: List[ObjectSpec]
+
+
+class Scene:
+    """scene::Scene { camera_location, objects } (src/scene.rs:5-8).
+
+    objects: list whose items are either a list of Plane/Sphere (a Vec<Box<dyn Primitive>>
+    aggregate) or a BoundingVolumeHierarchy."""
+
+    def __init__(self, camera_location, objects):
+        self.camera_location = tuple(float(c) for c in camera_location)
+        self.objects = list(objects)
+        self._spec = None
+        self._device_scenes = {}
+
+    def spec(self) -> SceneSpec:
+        if self._spec is None:
+            mats, mat_ids = [], {}
+
+            def mid(m):
+                if id(m) not in mat_ids:
+                    mat_ids[id(m)] = len(mats)
+                    if isinstance(m, ReflectiveMaterial):
+                        mats.append(MaterialSpec(N.MATERIAL_REFLECTIVE, m.colour, m.diffuse_strength,
+                                                 m.reflection_strength))
+                    elif isinstance(m, LambertianMaterial):
+                        mats.append(MaterialSpec(N.MATERIAL_LAMBERTIAN, m.colour, m.diffuse_strength, 0.0))
+                    else:
+                        raise TypeError(f"unsupported material {type(m).__name__}")
+                return mat_ids[id(m)]
+
+            meshes, objs = [], []
+            for o in self.objects:
+                if isinstance(o, BoundingVolumeHierarchy):
+                    meshes.append(MeshSpec(np.ascontiguousarray(o.mesh.vertices, dtype=np.float64),
+                                           np.ascontiguousarray(o.mesh.normals, dtype=np.float64),
+                                           mid(o.mesh.material)))
+                    objs.append(ObjectSpec("bvh", mesh=len(meshes) - 1))
+                else:
+                    prims = []
+                    for p in o:
+                        if isinstance(p, Plane):
+                            prims.append(PrimitiveSpec(N.PRIMITIVE_PLANE, mid(p.material), tuple(p.normal),
+                                                       float(p.distance_from_origin)))
+                        elif isinstance(p, Sphere):
+                            prims.append(PrimitiveSpec(N.PRIMITIVE_SPHERE, mid(p.material), tuple(p.centre),
+                                                       float(p.radius)))
+                        else:
+                            raise TypeError(f"unsupported primitive {type(p).__name__}")
+                    objs.append(ObjectSpec("primitives", prims))
+            self._spec = SceneSpec(self.camera_location, mats, meshes, objs)
+        return self._spec
+
+    def device_scene(self, device=0, host_only=False):
+        key = (device, host_only)
+        if key not in self._device_scenes:
+            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only)
+        return self._device_scenes[key]
+
+
+class DeviceScene:
+    """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
+
+    def __init__(self, spec: SceneSpec, device=0, host_only=False):
+        L = N.lib()
+        self.spec = spec
+        keep = []  # keep ctypes buffers alive during vr_scene_create
+        mats = (N.MaterialDesc * max(len(spec.materials), 1))()
+        for i, m in enumerate(spec.materials):
+            s = np.ascontiguousarray(m.colour.samples, dtype=np.float64)
+            keep.append(s)
+            mats[i] = N.MaterialDesc(m.kind, 0, N.Spectrum(m.colour.shortest_wavelength, m.colour.longest_wavelength,
+                                                           s.size, s.ctypes.data_as(C.POINTER(C.c_double))),
+                                     m.diffuse_strength, m.reflection_strength)
+        prims, objs, meshes = [], [], []
+        for o in spec.objects:
+            if o.kind == "primitives":
+                objs.append(N.ObjectDesc(N.OBJECT_PRIMITIVE_LIST, len(prims), len(o.primitives), 0))
+                for p in o.primitives:
+                    prims.append(N.PrimitiveDesc(p.kind, p.material, N.Vec3(*p.vector), p.scalar))
+            else:
+                objs.append(N.ObjectDesc(N.OBJECT_BVH, o.mesh, 1, 0))
+        for m in spec.meshes:
+            v = np.ascontiguousarray(m.vertices, dtype=np.float64).reshape(-1)
+            nn = np.ascontiguousarray(m.normals, dtype=np.float64).reshape(-1)
+            assert v.size == nn.size and v.size % 9 == 0
+            keep += [v, nn]
+            meshes.append(N.MeshDesc(v.size // 9, v.ctypes.data_as(C.POINTER(C.c_double)),
+                                     nn.ctypes.data_as(C.POINTER(C.c_double)), m.material, 0))
+        prim_arr = (N.PrimitiveDesc * max(len(prims), 1))(*prims)
+        obj_arr = (N.ObjectDesc * max(len(objs), 1))(*objs)
+        mesh_arr = (N.MeshDesc * max(len(meshes), 1))(*meshes)
+        desc = N.SceneDesc(N.Vec3(*spec.camera_location), len(spec.materials), len(prims), len(meshes), len(objs),
+                           mats, prim_arr, mesh_arr, obj_arr)
+        h = C.c_void_p()
+        N.check(L.vr_scene_create(C.byref(desc), device, N.SCENE_HOST_ONLY if host_only else 0, C.byref(h)))
+        self.handle = h
+        self.device = device
+        self.host_only = host_only
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            N.lib().vr_scene_destroy(h)
+            self.handle = None
+
+    def info(self):
+        i = N.SceneInfo()
+        N.check(N.lib().vr_scene_get_info(self.handle, C.byref(i)))
+        return {n: getattr(i, n) for n, _ in i._fields_}
+
+    def leaf_order(self, mesh):
+        out = np.zeros(len(self.spec.meshes[mesh].vertices), dtype=np.uint64)
+        N.check(N.lib().vr_scene_bvh_leaf_order(self.handle, mesh, out.ctypes.data_as(C.c_void_p)))
+        return out
