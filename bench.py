@@ -30,6 +30,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from vanrijn_amd import distributed as D  # noqa: E402
 from vanrijn_amd import scenes  # noqa: E402
 from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
 
@@ -108,11 +109,9 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step(i, timed=False):
-        first = (i * world + rank) * spp
-        st = render_tile_device(dscene, tile, H, W, spp, SEED, first, state.data_ptr(), stream.cuda_stream,
-                                timed=timed, device=local)
-        if world > 1:
-            dist.reduce(state, dst=0, op=dist.ReduceOp.SUM)
+        st = render_tile_device(dscene, tile, H, W, spp, SEED, D.first_sample(i, rank, world, spp), state.data_ptr(),
+                                stream.cuda_stream, timed=timed, device=local)
+        D.reduce_records(state)  # RCCL sum of the records onto rank 0 (no-op at N = 1)
         return st
 
     # counting launch (untimed): traversal counters of exactly this workload
@@ -167,7 +166,10 @@ def main():
                      "kernel": "render_kernel", "kernel_ms": round(avg_kernel_s * 1e3, 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests",
-                                                                    "rays", "shaded_triangle_hits", "samples")}},
+                                                                    "rays", "shaded_triangle_hits", "samples",
+                                                                    "traversal_slots", "path_loop_slots")},
+                     "traversal_lane_utilisation": round(counts["node_visits"] / max(1, counts["traversal_slots"]), 4),
+                     "path_loop_lane_utilisation": round(counts["rays"] / max(1, counts["path_loop_slots"]), 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds, args.cpu_threads)

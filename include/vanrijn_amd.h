@@ -193,6 +193,8 @@ typedef struct vr_launch_stats {
     uint64_t rays;
     uint64_t shaded_triangle_hits;
     uint64_t samples;
+    uint64_t traversal_slots;  /* 64 x wave-level traversal-loop iterations (lane utilisation) */
+    uint64_t path_loop_slots;  /* 64 x wave-level path-loop iterations */
 } vr_launch_stats;
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */

@@ -1,0 +1,508 @@
+// vr_device.h -- device-side building blocks of the gfx950 path tracer (included by vr_render.hip).
+//
+// f64 vector math, the counter-based random stream, spectra and CIE matching, the reference's
+// exact line-slab test, ray-triangle / sphere / plane tests, closest-hit traversal and hit
+// shading data.  Every expression follows the operation order of the reference's Rust source
+// (file:line cited per function) and is compiled with -ffp-contract=off, so decisions are
+// bit-identical to the oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vanrijn_amd.h"
+#include "rgb_spectrum_tables.h"
+#include "vr_layout.h"
+
+namespace vr {
+namespace dev {
+
+// ----------------------------------------------------------------------------------------------
+// f64 vector helpers in the reference's operation order (src/math/vec3.rs)
+// ----------------------------------------------------------------------------------------------
+struct V3 {
+    double x, y, z;
+};
+__device__ __forceinline__ V3 mk(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 scl(V3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+// vec3.rs:76-82 -- `Sum for f64` folds from -0.0
+__device__ __forceinline__ double dot(V3 a, V3 b) {
+    double s = -0.0;
+    s = s + a.x * b.x;
+    s = s + a.y * b.y;
+    s = s + a.z * b.z;
+    return s;
+}
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {  // vec3.rs:84-89
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ V3 normalize(V3 a) {  // vec3.rs:103-110 (multiply by 1/norm)
+    double inv = 1.0 / sqrt(dot(a, a));
+    return mk(a.x * inv, a.y * inv, a.z * inv);
+}
+__device__ __forceinline__ bool sgn(double x) { return __double_as_longlong(x) < 0; }
+__device__ __forceinline__ double sel(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+__device__ __forceinline__ V3 ldv(const double* p) { return mk(p[0], p[1], p[2]); }
+
+// ----------------------------------------------------------------------------------------------
+// Random stream "vr-splitmix v1" + rand 0.7 maps (same definition as oracle/vr_oracle.c)
+// ----------------------------------------------------------------------------------------------
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kSeedSalt = 0x76616E52696A6E31ull;
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+struct Rng {
+    uint64_t base;
+    uint64_t k;
+    __device__ __forceinline__ uint64_t next() {
+        k += 1;
+        return mix64(base + k * kGolden);
+    }
+    // rand 0.7 Standard f64 (camera.rs:49, photon.rs:21)
+    __device__ __forceinline__ double standard() { return (double)(next() >> 11) * 0x1.0p-53; }
+    // rand 0.7 Open01 f64 (lambertian_material.rs:39-48)
+    __device__ __forceinline__ double open01() {
+        return __longlong_as_double((long long)((next() >> 12) | 0x3FF0000000000000ull)) - (1.0 - 0x1.0p-53);
+    }
+};
+__device__ __forceinline__ uint64_t stream_base(uint64_t seed, uint64_t pixel, uint64_t sample) {
+    uint64_t k = mix64(seed ^ kSeedSalt);
+    k = mix64(k + pixel);
+    return mix64(k + sample);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Spectra (src/colour/spectrum.rs) and CIE matching (colour_xyz.rs:86-103)
+// ----------------------------------------------------------------------------------------------
+__constant__ double c_rgbspec[7][32] = VR_RGBSPEC_BASIS_INIT;
+
+// Spectrum::intensity_at_wavelength (spectrum.rs:64-79); sample(j) supplies samples[j]
+template <class F>
+__device__ __forceinline__ double spectrum_at(double shortest, double longest, int n, double wl, F sample) {
+    if (wl < shortest || wl > longest) return 0.0;
+    double range = longest - shortest;
+    int i = (int)((double)(n - 1) * ((wl - shortest) / range));  // `as usize` (wl >= shortest here)
+    double before = (double)i / (double)(n - 1) * range + shortest;
+    if (i == n - 1) return sample(i);
+    double after = (double)(i + 1) / (double)(n - 1) * range + shortest;
+    double delta = after - before;
+    double ratio = (wl - before) / delta;
+    return sample(i) * (1.0 - ratio) + sample(i + 1) * ratio;
+}
+
+__device__ __forceinline__ double material_colour(const Material* m, double wl) {
+    return spectrum_at(m->shortest, m->longest, m->n, wl, [&](int j) { return m->samples[j]; });
+}
+
+// test_lighting_environment (simple_random_integrator.rs:57-65): reflection_from_linear_rgb of
+// (w.y, w.y, 1) (spectrum.rs:81-165), evaluated only at the two samples the lookup needs.
+__device__ double sky_intensity(double wy, double wl) {
+    const double r = wy, g = wy, b = 1.0;
+    double c0, c1, c2;
+    int kx, ky;
+    if (r <= g && r <= b) {
+        if (g <= b) { c0 = r; c1 = g - r; c2 = b - g; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_BLUE; }
+        else { c0 = r; c1 = b - r; c2 = g - b; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_GREEN; }
+    } else if (g <= r && g < b) {
+        if (r <= b) { c0 = g; c1 = r - g; c2 = b - r; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_BLUE; }
+        else { c0 = g; c1 = b - g; c2 = r - b; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_RED; }
+    } else {
+        if (r <= g) { c0 = b; c1 = r - b; c2 = g - r; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_GREEN; }
+        else { c0 = b; c1 = g - b; c2 = r - g; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_RED; }
+    }
+    return spectrum_at(VR_RGBSPEC_SHORTEST, VR_RGBSPEC_LONGEST, 32, wl, [&](int j) {
+        return c0 * c_rgbspec[VR_RGBSPEC_WHITE][j] + c1 * c_rgbspec[kx][j] + c2 * c_rgbspec[ky][j];
+    });
+}
+
+__device__ __forceinline__ double gaussian(double wl, double alpha, double mu, double s1, double s2) {
+    double s = wl < mu ? s1 : s2;
+    double denominator = 2.0 * (s * s);
+    double t = wl - mu;
+    return alpha * exp(-(t * t) / denominator);
+}
+__device__ __forceinline__ V3 xyz_for_wavelength(double wl) {
+    return mk(gaussian(wl, 1.056, 599.8, 37.9, 31.0) + gaussian(wl, 0.362, 442.0, 16.0, 26.7) +
+                  gaussian(wl, -0.065, 501.1, 20.4, 26.2),
+              gaussian(wl, 0.821, 568.8, 46.9, 40.5) + gaussian(wl, 0.286, 530.9, 16.3, 31.1),
+              gaussian(wl, 1.217, 437.0, 11.8, 36.0) + gaussian(wl, 0.681, 459.0, 26.0, 13.8));
+}
+
+// ----------------------------------------------------------------------------------------------
+// Rays and primitives
+// ----------------------------------------------------------------------------------------------
+struct Ray {
+    V3 o, d;
+};
+// Per-ray constants hoisted out of every box / triangle test (bit-identical to recomputing them)
+struct RayPre {
+    V3 o, d, inv;
+    V3 pno;       // -origin, permuted (triangle.rs:37-40)
+    double sx, sy, pdz;
+    int k0, k1, k2;
+    bool exact_only;  // some |d_i| tiny or zero: every slab test takes the division path
+    bool behind_ok;   // |shear-axis component| large enough to cull boxes behind the origin
+};
+
+__device__ __forceinline__ RayPre prepare(const Ray& r) {
+    RayPre p;
+    p.o = r.o;
+    p.d = r.d;
+    p.inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    // indices_with_index_of_largest_element_last (triangle.rs:108-122): signed comparisons
+    int k0, k1, k2;
+    if (r.d.x > r.d.y) {
+        if (r.d.z > r.d.x) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 1; k1 = 2; k2 = 0; }
+    } else {
+        if (r.d.z > r.d.y) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 2; k1 = 0; k2 = 1; }
+    }
+    p.k0 = k0; p.k1 = k1; p.k2 = k2;
+    V3 no = neg(r.o);
+    p.pno = mk(sel(no, k0), sel(no, k1), sel(no, k2));
+    double pdx = sel(r.d, k0), pdy = sel(r.d, k1), pdz = sel(r.d, k2);
+    p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
+    p.sy = -pdy / pdz;
+    p.pdz = pdz;
+    const double tiny = 1e-150;
+    p.exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);
+    p.behind_ok = fabs(pdz) >= 0.01;
+    return p;
+}
+
+// raycasting/axis_aligned_bounding_box.rs:9-27 (+ util/interval.rs): the LINE slab test with
+// NaN-ignoring max/min.  The decision must equal the reference's division form bit for bit; the
+// common case is decided from reciprocal products (|error| <= ~3.3e-16 |t|) when the interval
+// is clearly non-empty or clearly empty, and only near-ties fall back to exact divisions.
+// Returns the (approximate) line interval for distance culling.
+__device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& tlo, double& thi) {
+    double lo = -INFINITY, hi = INFINITY;
+    {
+        double a = (b[0] - p.o.x) * p.inv.x, c = (b[1] - p.o.x) * p.inv.x;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        lo = fmax(lo, mn); hi = fmin(hi, mx);
+    }
+    {
+        double a = (b[2] - p.o.y) * p.inv.y, c = (b[3] - p.o.y) * p.inv.y;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        lo = fmax(lo, mn); hi = fmin(hi, mx);
+    }
+    {
+        double a = (b[4] - p.o.z) * p.inv.z, c = (b[5] - p.o.z) * p.inv.z;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        lo = fmax(lo, mn); hi = fmin(hi, mx);
+    }
+    tlo = lo;
+    thi = hi;
+    if (!p.exact_only) {
+        double err = 1e-15 * (fabs(lo) + fabs(hi));
+        if (hi - lo > err) return true;
+        if (lo - hi > err) return false;
+    }
+    // exact reference form (divisions)
+    double elo = -INFINITY, ehi = INFINITY;
+    {
+        double a = (b[0] - p.o.x) / p.d.x, c = (b[1] - p.o.x) / p.d.x;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
+    }
+    {
+        double a = (b[2] - p.o.y) / p.d.y, c = (b[3] - p.o.y) / p.d.y;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
+    }
+    {
+        double a = (b[4] - p.o.z) / p.d.z, c = (b[5] - p.o.z) / p.d.z;
+        double mn = a > c ? c : a, mx = a > c ? a : c;
+        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
+    }
+    if (p.exact_only) {
+        tlo = elo;
+        thi = ehi;
+    }
+    return !(elo > ehi);
+}
+
+// Triangle::intersect decision part (triangle.rs:35-66): returns distance, or -1 on a miss.
+// (A valid hit's distance is a norm, >= 0.)
+__device__ __forceinline__ double triangle_distance(const TriVerts& t, const RayPre& p, double bary[3]) {
+    V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
+    // translate by -origin, permute, shear (z unscaled)
+    double a0x = sel(v0, p.k0) + p.pno.x, a0y = sel(v0, p.k1) + p.pno.y, a0z = sel(v0, p.k2) + p.pno.z;
+    double a1x = sel(v1, p.k0) + p.pno.x, a1y = sel(v1, p.k1) + p.pno.y, a1z = sel(v1, p.k2) + p.pno.z;
+    double a2x = sel(v2, p.k0) + p.pno.x, a2y = sel(v2, p.k1) + p.pno.y, a2z = sel(v2, p.k2) + p.pno.z;
+    double t0x = a0x + p.sx * a0z, t0y = a0y + p.sy * a0z;
+    double t1x = a1x + p.sx * a1z, t1y = a1y + p.sy * a1z;
+    double t2x = a2x + p.sx * a2z, t2y = a2y + p.sy * a2z;
+    // signed_edge_functions (triangle.rs:141-158)
+    double e0 = t1x * t2y - t2x * t1y;
+    double e1 = t2x * t0y - t0x * t2y;
+    double e2 = t0x * t1y - t1x * t0y;
+    bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
+    if (!((!s0 && !s1 && !s2) || (s0 && s1 && s2))) return -1.0;
+    double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
+    double s = 0.0;
+    s = s + ea0;
+    s = s + ea1;
+    s = s + ea2;
+    double inv = 1.0 / s;
+    double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
+    double tz = 0.0;
+    tz = tz + a0z * b0;
+    tz = tz + a1z * b1;
+    tz = tz + a2z * b2;
+    if (sgn(tz) != sgn(p.pdz)) return -1.0;
+    V3 loc = mk(0.0, 0.0, 0.0);
+    loc = add(loc, scl(v0, b0));
+    loc = add(loc, scl(v1, b1));
+    loc = add(loc, scl(v2, b2));
+    V3 dv = sub(p.o, loc);
+    bary[0] = b0;
+    bary[1] = b1;
+    bary[2] = b2;
+    return sqrt(dot(dv, dv));
+}
+
+// Sphere::intersect (sphere.rs:39-93), decision part: distance or -1
+__device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p) {
+    V3 o = p.o, d = p.d, c = ldv(s.vec);
+    double a = 0.0;
+    a = a + d.x * d.x;
+    a = a + d.y * d.y;
+    a = a + d.z * d.z;
+    V3 bv = scl(sub(mk(o.x * d.x, o.y * d.y, o.z * d.z), mk(c.x * d.x, c.y * d.y, c.z * d.z)), 2.0);
+    double b = 0.0;
+    b = b + bv.x;
+    b = b + bv.y;
+    b = b + bv.z;
+    V3 cv = sub(add(mk(o.x * o.x, o.y * o.y, o.z * o.z), mk(c.x * c.x, c.y * c.y, c.z * c.z)),
+                scl(mk(c.x * o.x, c.y * o.y, c.z * o.z), 2.0));
+    double cc = 0.0;
+    cc = cc + cv.x;
+    cc = cc + cv.y;
+    cc = cc + cv.z;
+    cc = cc - s.scalar * s.scalar;
+    double delta_squared = b * b - 4.0 * a * cc;
+    if (delta_squared < 0.0) return -1.0;
+    double delta = sqrt(delta_squared);
+    double one_over_2_a = 1.0 / (2.0 * a);
+    double t1 = (-b - delta) * one_over_2_a;
+    double t2 = (-b + delta) * one_over_2_a;
+    double distance = (t1 < 0.0 || (t2 >= 0.0 && t1 >= t2)) ? t2 : t1;
+    if (distance <= 0.0) return -1.0;
+    return distance;
+}
+
+// Plane::intersect (plane.rs:49-75): t or -1 (t == 0 is a hit).  NaN t (ray inside the plane)
+// is reported as a hit with NaN distance, as in the reference; it never wins a comparison here.
+__device__ __forceinline__ bool plane_distance(const Prim& pl, const RayPre& p, double& t) {
+    V3 n = ldv(pl.vec);
+    double dn = dot(p.d, n);
+    V3 q = scl(n, pl.scalar);
+    double num = dot(sub(q, p.o), n);
+    if (dn == 0.0) {
+        if (num != 0.0) return false;
+    }
+    t = num / dn;
+    return !(t < 0.0);
+}
+
+struct HitInfo {
+    V3 loc, normal, tangent, cotangent, retro;
+    int material;
+};
+
+// full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96)
+__device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, HitInfo& h) {
+    double b[3];
+    triangle_distance(t, p, b);
+    V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
+    V3 loc = mk(0.0, 0.0, 0.0);
+    loc = add(loc, scl(v0, b[0]));
+    loc = add(loc, scl(v1, b[1]));
+    loc = add(loc, scl(v2, b[2]));
+    V3 ns = mk(0.0, 0.0, 0.0);
+    ns = add(ns, scl(mk(nn.n[0], nn.n[1], nn.n[2]), b[0]));
+    ns = add(ns, scl(mk(nn.n[3], nn.n[4], nn.n[5]), b[1]));
+    ns = add(ns, scl(mk(nn.n[6], nn.n[7], nn.n[8]), b[2]));
+    V3 n = normalize(ns);
+    V3 cot = normalize(cross(sub(v0, v1), n));
+    h.loc = loc;
+    h.normal = n;
+    h.cotangent = cot;
+    h.tangent = normalize(cross(cot, n));
+    h.retro = normalize(sub(p.o, loc));
+}
+
+__device__ void prim_info(const Prim& pr, const RayPre& p, double dist, HitInfo& h) {
+    h.material = pr.material;
+    if (pr.kind == 0) {  // plane.rs:66-74
+        h.loc = add(p.o, scl(p.d, dist));
+        h.normal = ldv(pr.vec);
+        h.tangent = ldv(pr.tan);
+        h.cotangent = ldv(pr.cot);
+        h.retro = neg(p.d);
+    } else {  // sphere.rs:71-90
+        V3 loc = add(p.o, scl(p.d, dist));
+        V3 n = normalize(sub(loc, ldv(pr.vec)));
+        V3 tan = normalize(cross(n, mk(0.0, 0.0, 1.0)));
+        h.loc = loc;
+        h.normal = n;
+        h.tangent = tan;
+        h.cotangent = cross(n, tan);
+        h.retro = neg(p.d);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Closest hit (sampler.rs:9-20 over vec_aggregate.rs:11-45 and bounding_volume_hierarchy.rs:77-120)
+// ----------------------------------------------------------------------------------------------
+enum HitKind : int { kNone = 0, kPrim = 1, kTri = 2 };
+struct Best {
+    double d;
+    int kind;
+    int index;   // prim index, or global leaf-ordered triangle index
+    int object;  // scene object index (ties between objects: the earlier object wins, min_by)
+    double bary[3];
+};
+
+struct Counts {
+    uint32_t box_tests, node_visits, tri_tests, rays, shaded;
+    uint32_t trav_slots, outer_slots;  // wave-level loop iterations x 64 (counted by one lane)
+};
+__device__ __forceinline__ bool first_active_lane() {
+    return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ void traverse_bvh(const DeviceScene& S, const Bvh& bvh, const RayPre& p, Best& best,
+                                             int* st_node, float* st_t, int tid, Counts& cnt) {
+    if (bvh.root == INT32_MIN) return;  // empty mesh: the reference's empty leaf never hits
+    const double margin = S.margin;
+    const double behind = S.behind_margin;
+    auto cull = [&](double tlo, double thi) {
+        double bound = best.kind ? best.d : INFINITY;
+        if (tlo > bound + margin * (1.0 + fabs(bound))) return true;
+        if (p.behind_ok && thi < -behind) return true;
+        return false;
+    };
+    // triangle candidate: distance ties go to the later leaf within this BVH (closest_intersection
+    // keeps `b` unless a.distance < b.distance, bounding_volume_hierarchy.rs:85) and to the
+    // earlier object across objects.
+    auto test_tri = [&](int tri) {  // global leaf-ordered triangle index
+        if (COUNT) cnt.tri_tests++;
+        double b[3];
+        double d = triangle_distance(S.tris[tri], p, b);
+        if (d < 0.0) return;
+        bool take;
+        if (!best.kind || d < best.d) take = true;
+        else if (d == best.d) take = (best.object == bvh.object) ? (tri > best.index) : (bvh.object < best.object);
+        else take = false;
+        if (take) {
+            best.d = d;
+            best.kind = kTri;
+            best.index = tri;
+            best.object = bvh.object;
+            best.bary[0] = b[0];
+            best.bary[1] = b[1];
+            best.bary[2] = b[2];
+        }
+    };
+    double tlo, thi;
+    if (COUNT) cnt.box_tests++;
+    if (!slab(bvh.root_box, p, tlo, thi) || cull(tlo, thi)) return;
+    if (bvh.root < 0) {
+        test_tri(~bvh.root);
+        return;
+    }
+    int node = bvh.root;
+    int sp = 0;
+    while (true) {
+        const Node& nd = S.nodes[node];
+        if (COUNT) {
+            cnt.node_visits++;
+            cnt.box_tests += 2;
+            if (first_active_lane()) cnt.trav_slots += 64;
+        }
+        double lo0, hi0, lo1, hi1;
+        const int c0 = nd.child[0], c1 = nd.child[1];
+        bool h0 = slab(nd.box[0], p, lo0, hi0) && !cull(lo0, hi0);
+        bool h1 = slab(nd.box[1], p, lo1, hi1) && !cull(lo1, hi1);
+        if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
+        if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
+        if (h0 && h1) {
+            int near = c0, far = c1;
+            double far_t = lo1;
+            if (lo1 < lo0) { near = c1; far = c0; far_t = lo0; }
+            st_node[sp * 256 + tid] = far;
+            st_t[sp * 256 + tid] = __double2float_rd(far_t);
+            ++sp;
+            node = near;
+            continue;
+        }
+        if (h0) { node = c0; continue; }
+        if (h1) { node = c1; continue; }
+        // pop, skipping entries the (possibly improved) best has since culled
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            double t = (double)st_t[sp * 256 + tid];
+            double bound = best.kind ? best.d : INFINITY;
+            if (t > bound + margin * (1.0 + fabs(bound))) continue;
+            node = st_node[sp * 256 + tid];
+            found = true;
+            break;
+        }
+        if (!found) break;
+    }
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ Best closest_hit(const DeviceScene& S, const RayPre& p, int* st_node, float* st_t, int tid,
+                                            Counts& cnt) {
+    Best best;
+    best.kind = kNone;
+    best.d = 0.0;
+    best.index = -1;
+    best.object = 0x7fffffff;
+    if (COUNT) cnt.rays++;
+    // primitive lists, in object then position order: a later equal distance never wins (min_by)
+    for (int i = 0; i < S.prim_count; ++i) {
+        const Prim& pr = S.prims[i];
+        double d;
+        bool ok;
+        if (pr.kind == 0) ok = plane_distance(pr, p, d);
+        else { d = sphere_distance(pr, p); ok = d >= 0.0; }
+        if (!ok) continue;
+        bool take = !best.kind || d < best.d;  // NaN never replaces, never gets replaced
+        if (take) {
+            best.d = d;
+            best.kind = kPrim;
+            best.index = i;
+            best.object = pr.object;
+        }
+    }
+    for (int b = 0; b < S.bvh_count; ++b) traverse_bvh<STACK, COUNT>(S, S.bvhs[b], p, best, st_node, st_t, tid, cnt);
+    return best;
+}
+
+__device__ __forceinline__ void hit_info(const DeviceScene& S, const Best& best, const RayPre& p, HitInfo& h) {
+    if (best.kind == kPrim) {
+        prim_info(S.prims[best.index], p, best.d, h);
+    } else {
+        triangle_info(S.tris[best.index], S.normals[best.index], p, h);
+        // material of the owning mesh
+        int m = 0;
+        for (int b = 0; b < S.bvh_count; ++b)
+            if (best.object == S.bvhs[b].object) m = S.bvhs[b].material;
+        h.material = m;
+    }
+}
+
+}  // namespace dev
+}  // namespace vr

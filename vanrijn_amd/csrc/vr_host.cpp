@@ -169,6 +169,7 @@ struct vr_scene {
     std::vector<int> mesh_tri_base;
     int max_depth = 0;
     uint32_t object_count = 0;
+    bool dark0 = true;  // every material's colour(0 nm) == 0: the recursion-limit photon needs no lambda-0 chain
     // device copies
     void* d_block = nullptr;
     size_t device_bytes = 0;
@@ -252,6 +253,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.records = nullptr;
     a.counters = nullptr;
     a.error_flag = s->d_error;
+    const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
+    a.shade_threshold = th ? (uint32_t)atoi(th) : 32u;
     return a;
 }
 
@@ -371,6 +374,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         dm.reflection = m.reflection_strength;
         std::memcpy(dm.samples, m.colour.samples, sizeof(double) * m.colour.sample_count);
         s->materials.push_back(dm);
+        if (vr_spectrum_intensity_at_wavelength(&m.colour, 0.0) != 0.0) s->dark0 = false;
     }
     // objects: primitive lists keep their order; BVHs are built per mesh
     std::vector<int> mesh_object(desc->mesh_count, -1);
@@ -545,7 +549,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         VR_HIP(hipEventCreate(&e1));
         VR_HIP(hipEventRecord(e0, st));
     }
-    int lr = vr::launch_render(a, stack_depth(s), counting, false, st);
+    int lr = vr::launch_render(a, stack_depth(s), counting, false, s->dark0, st);
     if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
     if (timed) {
         VR_HIP(hipEventRecord(e1, st));
@@ -569,6 +573,8 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
                 stats->rays = c[vr::kCntRays];
                 stats->shaded_triangle_hits = c[vr::kCntShadedTriangles];
                 stats->samples = c[vr::kCntSamples];
+                stats->traversal_slots = c[vr::kCntTraversalSlots];
+                stats->path_loop_slots = c[vr::kCntOuterSlots];
             }
         }
         return read_and_clear_error(s, st);
@@ -652,7 +658,7 @@ int vr_render_samples(const vr_scene* s, const vr_render_params* p, vr_sample_re
     q.accumulate = 0;
     vr::RenderArgs a = make_args(s, &q, (double*)cs.ptr);
     a.records = rec.ptr;
-    int lr = vr::launch_render(a, stack_depth(s), false, true, cs.stream);
+    int lr = vr::launch_render(a, stack_depth(s), false, true, s->dark0, cs.stream);
     if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
     VR_HIP(hipMemcpyAsync(out, rec.ptr, rec_bytes, hipMemcpyDeviceToHost, cs.stream));
     VR_HIP(hipStreamSynchronize(cs.stream));

@@ -89,6 +89,8 @@ struct RenderArgs {
     uint64_t seed, first_sample;
     uint32_t spp;
     uint32_t accumulate;
+    uint32_t shade_threshold;  // v2: lanes finished with traversal before the wave shades
+    uint32_t pad;
     double* state;             // [tile pixels][8]
     void* records;             // vr_sample_record* (record variant) or nullptr
     unsigned long long* counters;  // [8] (counting variant) or nullptr
@@ -111,11 +113,14 @@ enum Counter : int {
     kCntRays = 3,
     kCntShadedTriangles = 4,
     kCntSamples = 5,
+    kCntTraversalSlots = 6,  // 64 x wave-level traversal-loop iterations (lane-slot occupancy)
+    kCntOuterSlots = 7,      // 64 x wave-level path-loop iterations
     kCntCount = 8
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
-int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, void* stream);
+int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0,
+                  void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

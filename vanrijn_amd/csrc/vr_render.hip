@@ -22,500 +22,24 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/vanrijn_amd.h"
 #include "rgb_spectrum_tables.h"
 #include "vr_layout.h"
 
+#include "vr_device.h"
+
 namespace vr {
 namespace dev {
-
-// ----------------------------------------------------------------------------------------------
-// f64 vector helpers in the reference's operation order (src/math/vec3.rs)
-// ----------------------------------------------------------------------------------------------
-struct V3 {
-    double x, y, z;
-};
-__device__ __forceinline__ V3 mk(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 scl(V3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
-// vec3.rs:76-82 -- `Sum for f64` folds from -0.0
-__device__ __forceinline__ double dot(V3 a, V3 b) {
-    double s = -0.0;
-    s = s + a.x * b.x;
-    s = s + a.y * b.y;
-    s = s + a.z * b.z;
-    return s;
-}
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {  // vec3.rs:84-89
-    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ V3 normalize(V3 a) {  // vec3.rs:103-110 (multiply by 1/norm)
-    double inv = 1.0 / sqrt(dot(a, a));
-    return mk(a.x * inv, a.y * inv, a.z * inv);
-}
-__device__ __forceinline__ bool sgn(double x) { return __double_as_longlong(x) < 0; }
-__device__ __forceinline__ double sel(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
-__device__ __forceinline__ V3 ldv(const double* p) { return mk(p[0], p[1], p[2]); }
-
-// ----------------------------------------------------------------------------------------------
-// Random stream "vr-splitmix v1" + rand 0.7 maps (same definition as oracle/vr_oracle.c)
-// ----------------------------------------------------------------------------------------------
-constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
-constexpr uint64_t kSeedSalt = 0x76616E52696A6E31ull;
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-struct Rng {
-    uint64_t base;
-    uint64_t k;
-    __device__ __forceinline__ uint64_t next() {
-        k += 1;
-        return mix64(base + k * kGolden);
-    }
-    // rand 0.7 Standard f64 (camera.rs:49, photon.rs:21)
-    __device__ __forceinline__ double standard() { return (double)(next() >> 11) * 0x1.0p-53; }
-    // rand 0.7 Open01 f64 (lambertian_material.rs:39-48)
-    __device__ __forceinline__ double open01() {
-        return __longlong_as_double((long long)((next() >> 12) | 0x3FF0000000000000ull)) - (1.0 - 0x1.0p-53);
-    }
-};
-__device__ __forceinline__ uint64_t stream_base(uint64_t seed, uint64_t pixel, uint64_t sample) {
-    uint64_t k = mix64(seed ^ kSeedSalt);
-    k = mix64(k + pixel);
-    return mix64(k + sample);
-}
-
-// ----------------------------------------------------------------------------------------------
-// Spectra (src/colour/spectrum.rs) and CIE matching (colour_xyz.rs:86-103)
-// ----------------------------------------------------------------------------------------------
-__constant__ double c_rgbspec[7][32] = VR_RGBSPEC_BASIS_INIT;
-
-// Spectrum::intensity_at_wavelength (spectrum.rs:64-79); sample(j) supplies samples[j]
-template <class F>
-__device__ __forceinline__ double spectrum_at(double shortest, double longest, int n, double wl, F sample) {
-    if (wl < shortest || wl > longest) return 0.0;
-    double range = longest - shortest;
-    int i = (int)((double)(n - 1) * ((wl - shortest) / range));  // `as usize` (wl >= shortest here)
-    double before = (double)i / (double)(n - 1) * range + shortest;
-    if (i == n - 1) return sample(i);
-    double after = (double)(i + 1) / (double)(n - 1) * range + shortest;
-    double delta = after - before;
-    double ratio = (wl - before) / delta;
-    return sample(i) * (1.0 - ratio) + sample(i + 1) * ratio;
-}
-
-__device__ __forceinline__ double material_colour(const Material* m, double wl) {
-    return spectrum_at(m->shortest, m->longest, m->n, wl, [&](int j) { return m->samples[j]; });
-}
-
-// test_lighting_environment (simple_random_integrator.rs:57-65): reflection_from_linear_rgb of
-// (w.y, w.y, 1) (spectrum.rs:81-165), evaluated only at the two samples the lookup needs.
-__device__ double sky_intensity(double wy, double wl) {
-    const double r = wy, g = wy, b = 1.0;
-    double c0, c1, c2;
-    int kx, ky;
-    if (r <= g && r <= b) {
-        if (g <= b) { c0 = r; c1 = g - r; c2 = b - g; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_BLUE; }
-        else { c0 = r; c1 = b - r; c2 = g - b; kx = VR_RGBSPEC_CYAN; ky = VR_RGBSPEC_GREEN; }
-    } else if (g <= r && g < b) {
-        if (r <= b) { c0 = g; c1 = r - g; c2 = b - r; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_BLUE; }
-        else { c0 = g; c1 = b - g; c2 = r - b; kx = VR_RGBSPEC_MAGENTA; ky = VR_RGBSPEC_RED; }
-    } else {
-        if (r <= g) { c0 = b; c1 = r - b; c2 = g - r; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_GREEN; }
-        else { c0 = b; c1 = g - b; c2 = r - g; kx = VR_RGBSPEC_YELLOW; ky = VR_RGBSPEC_RED; }
-    }
-    return spectrum_at(VR_RGBSPEC_SHORTEST, VR_RGBSPEC_LONGEST, 32, wl, [&](int j) {
-        return c0 * c_rgbspec[VR_RGBSPEC_WHITE][j] + c1 * c_rgbspec[kx][j] + c2 * c_rgbspec[ky][j];
-    });
-}
-
-__device__ __forceinline__ double gaussian(double wl, double alpha, double mu, double s1, double s2) {
-    double s = wl < mu ? s1 : s2;
-    double denominator = 2.0 * (s * s);
-    double t = wl - mu;
-    return alpha * exp(-(t * t) / denominator);
-}
-__device__ __forceinline__ V3 xyz_for_wavelength(double wl) {
-    return mk(gaussian(wl, 1.056, 599.8, 37.9, 31.0) + gaussian(wl, 0.362, 442.0, 16.0, 26.7) +
-                  gaussian(wl, -0.065, 501.1, 20.4, 26.2),
-              gaussian(wl, 0.821, 568.8, 46.9, 40.5) + gaussian(wl, 0.286, 530.9, 16.3, 31.1),
-              gaussian(wl, 1.217, 437.0, 11.8, 36.0) + gaussian(wl, 0.681, 459.0, 26.0, 13.8));
-}
-
-// ----------------------------------------------------------------------------------------------
-// Rays and primitives
-// ----------------------------------------------------------------------------------------------
-struct Ray {
-    V3 o, d;
-};
-// Per-ray constants hoisted out of every box / triangle test (bit-identical to recomputing them)
-struct RayPre {
-    V3 o, d, inv;
-    V3 pno;       // -origin, permuted (triangle.rs:37-40)
-    double sx, sy, pdz;
-    int k0, k1, k2;
-    bool exact_only;  // some |d_i| tiny or zero: every slab test takes the division path
-    bool behind_ok;   // |shear-axis component| large enough to cull boxes behind the origin
-};
-
-__device__ __forceinline__ RayPre prepare(const Ray& r) {
-    RayPre p;
-    p.o = r.o;
-    p.d = r.d;
-    p.inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-    // indices_with_index_of_largest_element_last (triangle.rs:108-122): signed comparisons
-    int k0, k1, k2;
-    if (r.d.x > r.d.y) {
-        if (r.d.z > r.d.x) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 1; k1 = 2; k2 = 0; }
-    } else {
-        if (r.d.z > r.d.y) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 2; k1 = 0; k2 = 1; }
-    }
-    p.k0 = k0; p.k1 = k1; p.k2 = k2;
-    V3 no = neg(r.o);
-    p.pno = mk(sel(no, k0), sel(no, k1), sel(no, k2));
-    double pdx = sel(r.d, k0), pdy = sel(r.d, k1), pdz = sel(r.d, k2);
-    p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
-    p.sy = -pdy / pdz;
-    p.pdz = pdz;
-    const double tiny = 1e-150;
-    p.exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);
-    p.behind_ok = fabs(pdz) >= 0.01;
-    return p;
-}
-
-// raycasting/axis_aligned_bounding_box.rs:9-27 (+ util/interval.rs): the LINE slab test with
-// NaN-ignoring max/min.  The decision must equal the reference's division form bit for bit; the
-// common case is decided from reciprocal products (|error| <= ~3.3e-16 |t|) when the interval
-// is clearly non-empty or clearly empty, and only near-ties fall back to exact divisions.
-// Returns the (approximate) line interval for distance culling.
-__device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& tlo, double& thi) {
-    double lo = -INFINITY, hi = INFINITY;
-    {
-        double a = (b[0] - p.o.x) * p.inv.x, c = (b[1] - p.o.x) * p.inv.x;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    {
-        double a = (b[2] - p.o.y) * p.inv.y, c = (b[3] - p.o.y) * p.inv.y;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    {
-        double a = (b[4] - p.o.z) * p.inv.z, c = (b[5] - p.o.z) * p.inv.z;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    tlo = lo;
-    thi = hi;
-    if (!p.exact_only) {
-        double err = 1e-15 * (fabs(lo) + fabs(hi));
-        if (hi - lo > err) return true;
-        if (lo - hi > err) return false;
-    }
-    // exact reference form (divisions)
-    double elo = -INFINITY, ehi = INFINITY;
-    {
-        double a = (b[0] - p.o.x) / p.d.x, c = (b[1] - p.o.x) / p.d.x;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
-    }
-    {
-        double a = (b[2] - p.o.y) / p.d.y, c = (b[3] - p.o.y) / p.d.y;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
-    }
-    {
-        double a = (b[4] - p.o.z) / p.d.z, c = (b[5] - p.o.z) / p.d.z;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        elo = fmax(elo, mn); ehi = fmin(ehi, mx);
-    }
-    if (p.exact_only) {
-        tlo = elo;
-        thi = ehi;
-    }
-    return !(elo > ehi);
-}
-
-// Triangle::intersect decision part (triangle.rs:35-66): returns distance, or -1 on a miss.
-// (A valid hit's distance is a norm, >= 0.)
-__device__ __forceinline__ double triangle_distance(const TriVerts& t, const RayPre& p, double bary[3]) {
-    V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
-    // translate by -origin, permute, shear (z unscaled)
-    double a0x = sel(v0, p.k0) + p.pno.x, a0y = sel(v0, p.k1) + p.pno.y, a0z = sel(v0, p.k2) + p.pno.z;
-    double a1x = sel(v1, p.k0) + p.pno.x, a1y = sel(v1, p.k1) + p.pno.y, a1z = sel(v1, p.k2) + p.pno.z;
-    double a2x = sel(v2, p.k0) + p.pno.x, a2y = sel(v2, p.k1) + p.pno.y, a2z = sel(v2, p.k2) + p.pno.z;
-    double t0x = a0x + p.sx * a0z, t0y = a0y + p.sy * a0z;
-    double t1x = a1x + p.sx * a1z, t1y = a1y + p.sy * a1z;
-    double t2x = a2x + p.sx * a2z, t2y = a2y + p.sy * a2z;
-    // signed_edge_functions (triangle.rs:141-158)
-    double e0 = t1x * t2y - t2x * t1y;
-    double e1 = t2x * t0y - t0x * t2y;
-    double e2 = t0x * t1y - t1x * t0y;
-    bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
-    if (!((!s0 && !s1 && !s2) || (s0 && s1 && s2))) return -1.0;
-    double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
-    double s = 0.0;
-    s = s + ea0;
-    s = s + ea1;
-    s = s + ea2;
-    double inv = 1.0 / s;
-    double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
-    double tz = 0.0;
-    tz = tz + a0z * b0;
-    tz = tz + a1z * b1;
-    tz = tz + a2z * b2;
-    if (sgn(tz) != sgn(p.pdz)) return -1.0;
-    V3 loc = mk(0.0, 0.0, 0.0);
-    loc = add(loc, scl(v0, b0));
-    loc = add(loc, scl(v1, b1));
-    loc = add(loc, scl(v2, b2));
-    V3 dv = sub(p.o, loc);
-    bary[0] = b0;
-    bary[1] = b1;
-    bary[2] = b2;
-    return sqrt(dot(dv, dv));
-}
-
-// Sphere::intersect (sphere.rs:39-93), decision part: distance or -1
-__device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p) {
-    V3 o = p.o, d = p.d, c = ldv(s.vec);
-    double a = 0.0;
-    a = a + d.x * d.x;
-    a = a + d.y * d.y;
-    a = a + d.z * d.z;
-    V3 bv = scl(sub(mk(o.x * d.x, o.y * d.y, o.z * d.z), mk(c.x * d.x, c.y * d.y, c.z * d.z)), 2.0);
-    double b = 0.0;
-    b = b + bv.x;
-    b = b + bv.y;
-    b = b + bv.z;
-    V3 cv = sub(add(mk(o.x * o.x, o.y * o.y, o.z * o.z), mk(c.x * c.x, c.y * c.y, c.z * c.z)),
-                scl(mk(c.x * o.x, c.y * o.y, c.z * o.z), 2.0));
-    double cc = 0.0;
-    cc = cc + cv.x;
-    cc = cc + cv.y;
-    cc = cc + cv.z;
-    cc = cc - s.scalar * s.scalar;
-    double delta_squared = b * b - 4.0 * a * cc;
-    if (delta_squared < 0.0) return -1.0;
-    double delta = sqrt(delta_squared);
-    double one_over_2_a = 1.0 / (2.0 * a);
-    double t1 = (-b - delta) * one_over_2_a;
-    double t2 = (-b + delta) * one_over_2_a;
-    double distance = (t1 < 0.0 || (t2 >= 0.0 && t1 >= t2)) ? t2 : t1;
-    if (distance <= 0.0) return -1.0;
-    return distance;
-}
-
-// Plane::intersect (plane.rs:49-75): t or -1 (t == 0 is a hit).  NaN t (ray inside the plane)
-// is reported as a hit with NaN distance, as in the reference; it never wins a comparison here.
-__device__ __forceinline__ bool plane_distance(const Prim& pl, const RayPre& p, double& t) {
-    V3 n = ldv(pl.vec);
-    double dn = dot(p.d, n);
-    V3 q = scl(n, pl.scalar);
-    double num = dot(sub(q, p.o), n);
-    if (dn == 0.0) {
-        if (num != 0.0) return false;
-    }
-    t = num / dn;
-    return !(t < 0.0);
-}
-
-struct HitInfo {
-    V3 loc, normal, tangent, cotangent, retro;
-    int material;
-};
-
-// full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96)
-__device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, HitInfo& h) {
-    double b[3];
-    triangle_distance(t, p, b);
-    V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
-    V3 loc = mk(0.0, 0.0, 0.0);
-    loc = add(loc, scl(v0, b[0]));
-    loc = add(loc, scl(v1, b[1]));
-    loc = add(loc, scl(v2, b[2]));
-    V3 ns = mk(0.0, 0.0, 0.0);
-    ns = add(ns, scl(mk(nn.n[0], nn.n[1], nn.n[2]), b[0]));
-    ns = add(ns, scl(mk(nn.n[3], nn.n[4], nn.n[5]), b[1]));
-    ns = add(ns, scl(mk(nn.n[6], nn.n[7], nn.n[8]), b[2]));
-    V3 n = normalize(ns);
-    V3 cot = normalize(cross(sub(v0, v1), n));
-    h.loc = loc;
-    h.normal = n;
-    h.cotangent = cot;
-    h.tangent = normalize(cross(cot, n));
-    h.retro = normalize(sub(p.o, loc));
-}
-
-__device__ void prim_info(const Prim& pr, const RayPre& p, double dist, HitInfo& h) {
-    h.material = pr.material;
-    if (pr.kind == 0) {  // plane.rs:66-74
-        h.loc = add(p.o, scl(p.d, dist));
-        h.normal = ldv(pr.vec);
-        h.tangent = ldv(pr.tan);
-        h.cotangent = ldv(pr.cot);
-        h.retro = neg(p.d);
-    } else {  // sphere.rs:71-90
-        V3 loc = add(p.o, scl(p.d, dist));
-        V3 n = normalize(sub(loc, ldv(pr.vec)));
-        V3 tan = normalize(cross(n, mk(0.0, 0.0, 1.0)));
-        h.loc = loc;
-        h.normal = n;
-        h.tangent = tan;
-        h.cotangent = cross(n, tan);
-        h.retro = neg(p.d);
-    }
-}
-
-// ----------------------------------------------------------------------------------------------
-// Closest hit (sampler.rs:9-20 over vec_aggregate.rs:11-45 and bounding_volume_hierarchy.rs:77-120)
-// ----------------------------------------------------------------------------------------------
-enum HitKind : int { kNone = 0, kPrim = 1, kTri = 2 };
-struct Best {
-    double d;
-    int kind;
-    int index;   // prim index, or global leaf-ordered triangle index
-    int object;  // scene object index (ties between objects: the earlier object wins, min_by)
-    double bary[3];
-};
-
-struct Counts {
-    uint32_t box_tests, node_visits, tri_tests, rays, shaded;
-};
-
-template <int STACK, bool COUNT>
-__device__ __forceinline__ void traverse_bvh(const DeviceScene& S, const Bvh& bvh, const RayPre& p, Best& best,
-                                             int* st_node, float* st_t, int tid, Counts& cnt) {
-    if (bvh.root == INT32_MIN) return;  // empty mesh: the reference's empty leaf never hits
-    const double margin = S.margin;
-    const double behind = S.behind_margin;
-    auto cull = [&](double tlo, double thi) {
-        double bound = best.kind ? best.d : INFINITY;
-        if (tlo > bound + margin * (1.0 + fabs(bound))) return true;
-        if (p.behind_ok && thi < -behind) return true;
-        return false;
-    };
-    // triangle candidate: distance ties go to the later leaf within this BVH (closest_intersection
-    // keeps `b` unless a.distance < b.distance, bounding_volume_hierarchy.rs:85) and to the
-    // earlier object across objects.
-    auto test_tri = [&](int tri) {  // global leaf-ordered triangle index
-        if (COUNT) cnt.tri_tests++;
-        double b[3];
-        double d = triangle_distance(S.tris[tri], p, b);
-        if (d < 0.0) return;
-        bool take;
-        if (!best.kind || d < best.d) take = true;
-        else if (d == best.d) take = (best.object == bvh.object) ? (tri > best.index) : (bvh.object < best.object);
-        else take = false;
-        if (take) {
-            best.d = d;
-            best.kind = kTri;
-            best.index = tri;
-            best.object = bvh.object;
-            best.bary[0] = b[0];
-            best.bary[1] = b[1];
-            best.bary[2] = b[2];
-        }
-    };
-    double tlo, thi;
-    if (COUNT) cnt.box_tests++;
-    if (!slab(bvh.root_box, p, tlo, thi) || cull(tlo, thi)) return;
-    if (bvh.root < 0) {
-        test_tri(~bvh.root);
-        return;
-    }
-    int node = bvh.root;
-    int sp = 0;
-    while (true) {
-        const Node& nd = S.nodes[node];
-        if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
-        double lo0, hi0, lo1, hi1;
-        const int c0 = nd.child[0], c1 = nd.child[1];
-        bool h0 = slab(nd.box[0], p, lo0, hi0) && !cull(lo0, hi0);
-        bool h1 = slab(nd.box[1], p, lo1, hi1) && !cull(lo1, hi1);
-        if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
-        if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
-        if (h0 && h1) {
-            int near = c0, far = c1;
-            double far_t = lo1;
-            if (lo1 < lo0) { near = c1; far = c0; far_t = lo0; }
-            st_node[sp * 256 + tid] = far;
-            st_t[sp * 256 + tid] = __double2float_rd(far_t);
-            ++sp;
-            node = near;
-            continue;
-        }
-        if (h0) { node = c0; continue; }
-        if (h1) { node = c1; continue; }
-        // pop, skipping entries the (possibly improved) best has since culled
-        bool found = false;
-        while (sp > 0) {
-            --sp;
-            double t = (double)st_t[sp * 256 + tid];
-            double bound = best.kind ? best.d : INFINITY;
-            if (t > bound + margin * (1.0 + fabs(bound))) continue;
-            node = st_node[sp * 256 + tid];
-            found = true;
-            break;
-        }
-        if (!found) break;
-    }
-}
-
-template <int STACK, bool COUNT>
-__device__ __forceinline__ Best closest_hit(const DeviceScene& S, const RayPre& p, int* st_node, float* st_t, int tid,
-                                            Counts& cnt) {
-    Best best;
-    best.kind = kNone;
-    best.d = 0.0;
-    best.index = -1;
-    best.object = 0x7fffffff;
-    if (COUNT) cnt.rays++;
-    // primitive lists, in object then position order: a later equal distance never wins (min_by)
-    for (int i = 0; i < S.prim_count; ++i) {
-        const Prim& pr = S.prims[i];
-        double d;
-        bool ok;
-        if (pr.kind == 0) ok = plane_distance(pr, p, d);
-        else { d = sphere_distance(pr, p); ok = d >= 0.0; }
-        if (!ok) continue;
-        bool take = !best.kind || d < best.d;  // NaN never replaces, never gets replaced
-        if (take) {
-            best.d = d;
-            best.kind = kPrim;
-            best.index = i;
-            best.object = pr.object;
-        }
-    }
-    for (int b = 0; b < S.bvh_count; ++b) traverse_bvh<STACK, COUNT>(S, S.bvhs[b], p, best, st_node, st_t, tid, cnt);
-    return best;
-}
-
-__device__ __forceinline__ void hit_info(const DeviceScene& S, const Best& best, const RayPre& p, HitInfo& h) {
-    if (best.kind == kPrim) {
-        prim_info(S.prims[best.index], p, best.d, h);
-    } else {
-        triangle_info(S.tris[best.index], S.normals[best.index], p, h);
-        // material of the owning mesh
-        int m = 0;
-        for (int b = 0; b < S.bvh_count; ++b)
-            if (best.object == S.bvhs[b].object) m = S.bvhs[b].material;
-        h.material = m;
-    }
-}
 
 // ----------------------------------------------------------------------------------------------
 // Kernels
 // ----------------------------------------------------------------------------------------------
 __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}; }  // mod.rs:41-46
 
-template <int STACK, bool COUNT, bool RECORD>
-__global__ __launch_bounds__(256) void render_kernel(RenderArgs A) {
+template <int STACK, bool COUNT, bool RECORD, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void render_kernel_v1(RenderArgs A) {
     __shared__ int st_node[STACK * 256];
     __shared__ float st_t[STACK * 256];
     const int tid = threadIdx.x;
@@ -527,7 +51,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderArgs A) {
     const uint64_t py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool live = px < A.tile_width && py < A.tile_height;
     const DeviceScene& S = A.scene;
-    Counts cnt = {0, 0, 0, 0, 0};
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     uint32_t samples_done = 0;
 
     const uint64_t row = A.start_row + py, col = A.start_column + px;
@@ -584,6 +108,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderArgs A) {
     };
 
     while (active) {
+        if (COUNT && first_active_lane()) cnt.outer_slots += 64;
         if (need_camera) {
             if (s_idx == A.spp) { active = false; break; }
             rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
@@ -715,6 +240,333 @@ __global__ __launch_bounds__(256) void render_kernel(RenderArgs A) {
         atomicAdd(&A.counters[kCntRays], (unsigned long long)cnt.rays);
         atomicAdd(&A.counters[kCntShadedTriangles], (unsigned long long)cnt.shaded);
         atomicAdd(&A.counters[kCntSamples], (unsigned long long)samples_done);
+        atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
+        atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Render kernel v2: one pixel per lane, traversal and shading interleaved by phases.
+//
+// v1 (render_kernel_v1) traces one ray per lane per path-loop iteration, so a wave's traversal
+// loop runs as long as its longest ray (measured lane utilisation 25 %).  v2 keeps each lane's
+// traversal state (node, LDS stack, closest hit so far) alive across iterations: the wave steps
+// nodes for all traversing lanes until at least `shade_threshold` lanes have finished, then those
+// lanes shade (BSDF, next bounce ray or sample end + next camera ray) and rejoin the traversal
+// while the unfinished lanes resume where they stopped.  Kahan sums live in LDS, the stack holds
+// node indices only (a popped subtree is culled by its children's box tests), which keeps the
+// kernel at 4 workgroups (16 waves) per CU.
+// ----------------------------------------------------------------------------------------------
+enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
+
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
+    __shared__ uint32_t st_node[STACK * 256];
+    __shared__ double kahan[8 * 256];  // [sum x, sum y, sum z, bias x, bias y, bias z, weight, weight_bias][tid]
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint64_t bx = blockIdx.x % ((A.tile_width + 15) / 16);
+    const uint64_t by = blockIdx.x / ((A.tile_width + 15) / 16);
+    const uint64_t px = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint64_t py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool live = px < A.tile_width && py < A.tile_height;
+    const DeviceScene& S = A.scene;
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t samples_done = 0;
+    const uint64_t row = A.start_row + py, col = A.start_column + px;
+    const uint64_t pix = py * A.tile_width + px;
+    for (int k = 0; k < 8; ++k) kahan[k * 256 + tid] = (live && A.accumulate) ? A.state[pix * 8 + k] : 0.0;
+
+    const double fw_d = (double)A.width, fh_d = (double)A.height;
+    double film_w, film_h;
+    if (fw_d > fh_d) { film_w = fw_d / fh_d; film_h = 1.0; } else { film_w = 1.0; film_h = fw_d / fh_d; }
+    const double pixel_w = film_w * (1.0 / fw_d), pixel_h = film_h * (1.0 / fh_d);
+
+    int state = (live && A.spp > 0) ? kNeedRay : kDone;
+    uint32_t s_idx = 0;
+    Rng rng;
+    rng.base = 0;
+    rng.k = 0;
+    RayPre pre;
+    Best best;
+    int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
+    int depth = -1, bounces = 0, flags = 0;
+    double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
+
+    // the BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
+    auto culled = [&](double tlo, double thi) {
+        double bound = best.kind ? best.d : INFINITY;
+        if (tlo > bound + S.margin * (1.0 + fabs(bound))) return true;
+        if (pre.behind_ok && thi < -S.behind_margin) return true;
+        return false;
+    };
+    auto test_tri = [&](int tri) {
+        if (COUNT) cnt.tri_tests++;
+        double b[3];
+        double d = triangle_distance(S.tris[tri], pre, b);
+        if (d < 0.0) return;
+        bool take;
+        if (!best.kind || d < best.d) take = true;
+        else if (d == best.d) take = (best.object == cur_object) ? (tri > best.index) : (cur_object < best.object);
+        else take = false;
+        if (take) {
+            best.d = d;
+            best.kind = kTri;
+            best.index = tri;
+            best.object = cur_object;
+        }
+    };
+    // find the next BVH (from bvh_i) with work: returns false when the ray is fully traced
+    auto start_bvhs = [&]() {
+        for (; bvh_i < S.bvh_count; ++bvh_i) {
+            const Bvh& bvh = S.bvhs[bvh_i];
+            if (bvh.root == INT32_MIN) continue;
+            cur_object = bvh.object;
+            double lo, hi;
+            if (COUNT) cnt.box_tests++;
+            if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
+            if (bvh.root < 0) {
+                test_tri(~bvh.root);
+                continue;
+            }
+            node = bvh.root;
+            sp = 0;
+            return true;
+        }
+        return false;
+    };
+    // a new ray: analytic primitives first (object then position order), then the BVHs
+    auto begin_ray = [&](V3 o, V3 d) {
+        pre = prepare(Ray{o, d});
+        if (COUNT) cnt.rays++;
+        best.kind = kNone;
+        best.d = 0.0;
+        best.index = -1;
+        best.object = 0x7fffffff;
+        for (int i = 0; i < S.prim_count; ++i) {
+            const Prim& pr = S.prims[i];
+            double dd;
+            bool ok;
+            if (pr.kind == 0) ok = plane_distance(pr, pre, dd);
+            else { dd = sphere_distance(pr, pre); ok = dd >= 0.0; }
+            if (ok && (!best.kind || dd < best.d)) {
+                best.d = dd;
+                best.kind = kPrim;
+                best.index = i;
+                best.object = pr.object;
+            }
+        }
+        bvh_i = 0;
+        node = -1;
+        state = start_bvhs() ? kTraversing : kTraversed;
+    };
+    auto finish = [&](double wl, double I) {  // update_pixel(row, col, photon x 360, 1.0)
+        double Is = I * 360.0;
+        V3 c = xyz_for_wavelength(wl);
+        double cx = c.x * Is, cy = c.y * Is, cz = c.z * Is;
+        double* K = kahan + tid;
+        double wsum = K[6 * 256], wbias = K[7 * 256];
+        double wy = 1.0 - wbias;
+        double wt = wsum + wy;
+        K[7 * 256] = (wt - wsum) - wy;
+        K[6 * 256] = wt;
+        const double cc[3] = {cx, cy, cz};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double sum = K[k * 256], bias = K[(3 + k) * 256];
+            double y = cc[k] * 1.0 - bias;
+            double t = sum + y;
+            K[(3 + k) * 256] = (t - sum) - y;
+            K[k * 256] = t;
+        }
+        if (RECORD) {
+            vr_sample_record* rec = (vr_sample_record*)A.records + (pix * A.spp + s_idx);
+            rec->wavelength = wl;
+            rec->intensity = I;
+            rec->xyz[0] = cx;
+            rec->xyz[1] = cy;
+            rec->xyz[2] = cz;
+            rec->bounces = bounces;
+            rec->flags = flags;
+        }
+        if (COUNT) samples_done++;
+        ++s_idx;
+        state = kNeedRay;
+    };
+
+    while (true) {
+        // ---------------------------------------------------------------- phase A: shade
+        if (COUNT && first_active_lane()) cnt.outer_slots += 64;
+        if (state == kTraversed) {
+            bool shade = false;
+            if (depth < 0) {
+                if (!best.kind) {
+                    finish(0.0, 0.0);  // camera.rs:110-113
+                } else {
+                    flags |= 1;
+                    lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
+                    T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0; b0 = 0.0;
+                    depth = 0;
+                    shade = true;
+                }
+            } else if (!best.kind) {
+                finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
+            } else {
+                depth += 1;
+                if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
+                    flags |= 2;
+                    finish(0.0, DARK0 ? b0 : Acc0);
+                } else {
+                    shade = true;
+                }
+            }
+            if (shade) {
+                HitInfo h;
+                hit_info(S, best, pre, h);
+                if (COUNT && best.kind == kTri) cnt.shaded++;
+                const double m00 = h.tangent.x, m01 = h.tangent.y, m02 = h.tangent.z;
+                const double m10 = h.cotangent.x, m11 = h.cotangent.y, m12 = h.cotangent.z;
+                const double m20 = h.normal.x, m21 = h.normal.y, m22 = h.normal.z;
+                const double mi00 = m11 * m22 - m12 * m21, mi01 = m10 * m22 - m12 * m20, mi02 = m10 * m21 - m11 * m20;
+                const double mi10 = m01 * m22 - m02 * m21, mi11 = m00 * m22 - m02 * m20, mi12 = m00 * m21 - m01 * m20;
+                const double mi20 = m01 * m12 - m02 * m11, mi21 = m00 * m12 - m02 * m10, mi22 = m00 * m11 - m01 * m10;
+                const double det = m00 * mi00 - m01 * mi01 + m02 * mi02;
+                if (det == 0.0) {  // the reference panics ("Expected matrix to be invertable.")
+                    flags |= 4;
+                    atomicOr(A.error_flag, 1);
+                    finish(0.0, 0.0);
+                } else {
+                    const V3 w_i = mk(dot(h.tangent, h.retro), dot(h.cotangent, h.retro), dot(h.normal, h.retro));
+                    const Material* mat = &S.materials[h.material];
+                    V3 w_o;
+                    double pdf;
+                    if (mat->kind == 1) {  // reflective_material.rs:42-47
+                        w_o = mk(-w_i.x, -w_i.y, w_i.z);
+                        pdf = 1.0;
+                    } else {  // lambertian_material.rs:36-59
+                        double x = 2.0 * rng.open01() - 1.0;
+                        double y = 2.0 * rng.open01() - 1.0;
+                        while (dot(mk(x, y, 0.0), mk(x, y, 0.0)) > 1.0) {
+                            x = 2.0 * rng.open01() - 1.0;
+                            y = 2.0 * rng.open01() - 1.0;
+                        }
+                        double z = fmax(sqrt(1.0 - x * x - y * y), 0.0);
+                        V3 w = mk(x, y, z);
+                        double cos_theta = dot(w, mk(0.0, 0.0, 1.0));
+                        double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+                        w_o = normalize(w);
+                        pdf = (cos_theta * sin_theta) / 3.14159265358979323846;
+                    }
+                    // bsdf_to_world = cofactor^T * det (mat3.rs:111-118)
+                    const V3 inv0 = mk((1.0 * mi00) * det, (-1.0 * mi10) * det, (1.0 * mi20) * det);
+                    const V3 inv1 = mk((-1.0 * mi01) * det, (1.0 * mi11) * det, (-1.0 * mi21) * det);
+                    const V3 inv2 = mk((1.0 * mi02) * det, (-1.0 * mi12) * det, (1.0 * mi22) * det);
+                    const V3 wo_world = mk(dot(inv0, w_o), dot(inv1, w_o), dot(inv2, w_o));
+                    const double cosf = fabs(dot(wo_world, h.normal));
+                    const double c_l = material_colour(mat, lambda);
+                    const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
+                    double a, a0, bterm;
+                    if (mat->kind == 1) {  // reflective_material.rs:17-39
+                        if (w_i.z <= 0.0 || w_o.z <= 0.0) {
+                            a = 0.0; a0 = 0.0; bterm = 0.0;
+                        } else {
+                            V3 refl = mk(-w_o.x, -w_o.y, w_o.z);
+                            double cth = dot(w_i, refl);
+                            cth = cth < 0.0 ? 0.0 : (cth > 1.0 ? 1.0 : cth);
+                            double theta = acos(fabs(cth));
+                            const double sigma = 0.05, two = 2.0;
+                            double f = mat->reflection * exp(-(pow(theta, two)) / (two * sigma * sigma));
+                            a = (((pdf * cosf) * c_l) * mat->diffuse) * (1.0 - f);
+                            a0 = (((pdf * cosf) * c_0) * mat->diffuse) * (1.0 - f);
+                            bterm = f;
+                        }
+                    } else {  // lambertian_material.rs:27-34
+                        a = ((pdf * cosf) * c_l) * mat->diffuse;
+                        a0 = ((pdf * cosf) * c_0) * mat->diffuse;
+                        bterm = 0.0;
+                    }
+                    if (depth == 0) b0 = bterm;
+                    Acc = Acc + T * bterm;
+                    T = T * a;
+                    if (!DARK0) {
+                        Acc0 = Acc0 + T0 * bterm;
+                        T0 = T0 * a0;
+                    }
+                    const bool zero_tail = DARK0 ? (b0 == 0.0) : (T0 == 0.0 && Acc0 == 0.0);
+                    if (!RECORD && T == 0.0 && Acc == 0.0 && zero_tail) {
+                        finish(lambda, 0.0);  // every continuation yields intensity 0
+                    } else {
+                        // Ray::new(location, w_o).bias(1e-7) (mod.rs:41-61)
+                        wo_y = wo_world.y;
+                        V3 d1 = normalize(wo_world);
+                        ++bounces;
+                        begin_ray(add(h.loc, scl(d1, kBounceBias)), normalize(d1));
+                    }
+                }
+            }
+        }
+        if (state == kNeedRay) {
+            if (s_idx == A.spp) {
+                state = kDone;
+            } else {
+                rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
+                rng.k = 0;
+                double ux = rng.standard();  // camera.rs:52-66: x's draw first
+                double uy = rng.standard();
+                double x = ((double)col + ux) * pixel_w - film_w * 0.5;
+                double y = ((double)(A.height - (row + 1)) + uy) * pixel_h - film_h * 0.5;
+                depth = -1;
+                bounces = 0;
+                flags = 0;
+                begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
+            }
+        }
+        if (__ballot(state != kDone) == 0) break;
+        // ---------------------------------------------------------------- phase B: traverse
+        do {
+            if (COUNT && first_active_lane()) cnt.trav_slots += 64;
+            if (state == kTraversing) {
+                const Node& nd = S.nodes[node];
+                if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
+                double lo0, hi0, lo1, hi1;
+                const int c0 = nd.child[0], c1 = nd.child[1];
+                bool h0 = slab(nd.box[0], pre, lo0, hi0) && !culled(lo0, hi0);
+                bool h1 = slab(nd.box[1], pre, lo1, hi1) && !culled(lo1, hi1);
+                if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
+                if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
+                if (h0 && h1) {
+                    int near = c0, far = c1;
+                    if (lo1 < lo0) { near = c1; far = c0; }
+                    st_node[sp * 256 + tid] = (uint32_t)far;
+                    ++sp;
+                    node = near;
+                } else if (h0) {
+                    node = c0;
+                } else if (h1) {
+                    node = c1;
+                } else if (sp > 0) {
+                    --sp;
+                    node = (int)st_node[sp * 256 + tid];
+                } else {
+                    ++bvh_i;
+                    if (!start_bvhs()) state = kTraversed;
+                }
+            }
+        } while (__ballot(state == kTraversing) != 0 &&
+                 __popcll(__ballot(state == kTraversed)) < (int)A.shade_threshold);
+    }
+
+    if (live)
+        for (int k = 0; k < 8; ++k) A.state[pix * 8 + k] = kahan[k * 256 + tid];
+    if (COUNT) {
+        atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
+        atomicAdd(&A.counters[kCntNodeVisits], (unsigned long long)cnt.node_visits);
+        atomicAdd(&A.counters[kCntTriangleTests], (unsigned long long)cnt.tri_tests);
+        atomicAdd(&A.counters[kCntRays], (unsigned long long)cnt.rays);
+        atomicAdd(&A.counters[kCntShadedTriangles], (unsigned long long)cnt.shaded);
+        atomicAdd(&A.counters[kCntSamples], (unsigned long long)samples_done);
+        atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
+        atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
     }
 }
 
@@ -729,7 +581,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
     r.o = ldv(A.origins + 3 * i);
     r.d = ldv(A.directions + 3 * i);
     RayPre pre = prepare(r);
-    Counts cnt = {0, 0, 0, 0, 0};
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     Best best = closest_hit<STACK, false>(A.scene, pre, st_node, st_t, tid, cnt);
     vr_hit_record* out = (vr_hit_record*)A.out + i;
     out->valid = best.kind != kNone;
@@ -756,22 +608,44 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
 // Host-side launch wrappers
 // ----------------------------------------------------------------------------------------------
 template <int STACK>
-static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, hipStream_t s) {
+static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, hipStream_t s) {
     const uint64_t blocks = ((a.tile_width + 15) / 16) * ((a.tile_height + 15) / 16);
     dim3 grid((unsigned)blocks), block(256);
-    if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true>), grid, block, 0, s, a);
-    else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((dev::render_kernel<STACK, false, false>), grid, block, 0, s, a);
+    // experiment hook (tools/variants.py): 1 = v1 kernel, 2/3/4 = v2 with that many waves per SIMD
+    const char* ve = getenv("VR_KERNEL_VARIANT");
+    const int variant = ve ? atoi(ve) : 0;
+    if (variant == 1 && !recording) {
+        if (counting) hipLaunchKernelGGL((dev::render_kernel_v1<STACK, true, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((dev::render_kernel_v1<STACK, false, false>), grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+    if (variant >= 2 && variant <= 4 && !recording && !counting && dark0) {
+        if (variant == 2) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 2>), grid, block, 0, s, a);
+        if (variant == 3) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3>), grid, block, 0, s, a);
+        if (variant == 4) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 4>), grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+#define VR_LAUNCH(C, R, D) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D>), grid, block, 0, s, a)
+    if (dark0) {
+        if (recording) VR_LAUNCH(false, true, true);
+        else if (counting) VR_LAUNCH(true, false, true);
+        else VR_LAUNCH(false, false, true);
+    } else {
+        if (recording) VR_LAUNCH(false, true, false);
+        else if (counting) VR_LAUNCH(true, false, false);
+        else VR_LAUNCH(false, false, false);
+    }
+#undef VR_LAUNCH
     return hipGetLastError();
 }
 
-int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, void* stream) {
+int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (a.tile_width == 0 || a.tile_height == 0) return 0;
     hipError_t e;
-    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, s);
-    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, s);
-    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, s);
+    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, s);
+    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, s);
+    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, s);
     else return -1000;
     return (int)e;
 }
