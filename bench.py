@@ -167,7 +167,8 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests",
                                                                     "rays", "shaded_triangle_hits", "samples",
-                                                                    "traversal_slots", "path_loop_slots")},
+                                                                    "traversal_slots", "path_loop_slots",
+                                                                    "exact_box_tests")},
                      "traversal_lane_utilisation": round(counts["node_visits"] / max(1, counts["traversal_slots"]), 4),
                      "path_loop_lane_utilisation": round(counts["rays"] / max(1, counts["path_loop_slots"]), 4)},
     }

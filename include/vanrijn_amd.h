@@ -195,6 +195,7 @@ typedef struct vr_launch_stats {
     uint64_t samples;
     uint64_t traversal_slots;  /* 64 x wave-level traversal-loop iterations (lane utilisation) */
     uint64_t path_loop_slots;  /* 64 x wave-level path-loop iterations */
+    uint64_t exact_box_tests;  /* f32 box tests too close to call, re-run exactly in f64 */
 } vr_launch_stats;
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */

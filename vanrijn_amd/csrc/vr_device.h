@@ -143,11 +143,15 @@ struct Ray {
 // Per-ray constants hoisted out of every box / triangle test (bit-identical to recomputing them)
 struct RayPre {
     V3 o, d, inv;
-    V3 pno;       // -origin, permuted (triangle.rs:37-40)
     double sx, sy, pdz;
-    int k0, k1, k2;
-    bool exact_only;  // some |d_i| tiny or zero: every slab test takes the division path
-    bool behind_ok;   // |shear-axis component| large enough to cull boxes behind the origin
+    int flags;  // bits 0-1: axis rotation r (permutation [r, r+1, r+2] mod 3); bit 2: exact_only
+                // (some |d_i| tiny or zero: every slab takes the division path); bit 3: behind_ok
+                // (|shear-axis component| >= 0.01: boxes behind the origin may be culled)
+    __device__ __forceinline__ int k0() const { return flags & 3; }
+    __device__ __forceinline__ int k1() const { int k = (flags & 3) + 1; return k == 3 ? 0 : k; }
+    __device__ __forceinline__ int k2() const { int k = (flags & 3) + 2; return k >= 3 ? k - 3 : k; }
+    __device__ __forceinline__ bool exact_only() const { return (flags & 4) != 0; }
+    __device__ __forceinline__ bool behind_ok() const { return (flags & 8) != 0; }
 };
 
 __device__ __forceinline__ RayPre prepare(const Ray& r) {
@@ -155,23 +159,19 @@ __device__ __forceinline__ RayPre prepare(const Ray& r) {
     p.o = r.o;
     p.d = r.d;
     p.inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-    // indices_with_index_of_largest_element_last (triangle.rs:108-122): signed comparisons
-    int k0, k1, k2;
-    if (r.d.x > r.d.y) {
-        if (r.d.z > r.d.x) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 1; k1 = 2; k2 = 0; }
-    } else {
-        if (r.d.z > r.d.y) { k0 = 0; k1 = 1; k2 = 2; } else { k0 = 2; k1 = 0; k2 = 1; }
-    }
-    p.k0 = k0; p.k1 = k1; p.k2 = k2;
-    V3 no = neg(r.o);
-    p.pno = mk(sel(no, k0), sel(no, k1), sel(no, k2));
+    // indices_with_index_of_largest_element_last (triangle.rs:108-122): signed comparisons;
+    // the three outcomes [0,1,2], [1,2,0], [2,0,1] are the rotations r = 0, 1, 2
+    int rot;
+    if (r.d.x > r.d.y) rot = (r.d.z > r.d.x) ? 0 : 1;
+    else rot = (r.d.z > r.d.y) ? 0 : 2;
+    const int k0 = rot, k1 = rot == 2 ? 0 : rot + 1, k2 = rot == 0 ? 2 : rot - 1;
     double pdx = sel(r.d, k0), pdy = sel(r.d, k1), pdz = sel(r.d, k2);
     p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
     p.sy = -pdy / pdz;
     p.pdz = pdz;
     const double tiny = 1e-150;
-    p.exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);
-    p.behind_ok = fabs(pdz) >= 0.01;
+    const bool exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);
+    p.flags = rot | (exact_only ? 4 : 0) | (fabs(pdz) >= 0.01 ? 8 : 0);
     return p;
 }
 
@@ -199,7 +199,7 @@ __device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& t
     }
     tlo = lo;
     thi = hi;
-    if (!p.exact_only) {
+    if (!p.exact_only()) {
         double err = 1e-15 * (fabs(lo) + fabs(hi));
         if (hi - lo > err) return true;
         if (lo - hi > err) return false;
@@ -221,47 +221,86 @@ __device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& t
         double mn = a > c ? c : a, mx = a > c ? a : c;
         elo = fmax(elo, mn); ehi = fmin(ehi, mx);
     }
-    if (p.exact_only) {
+    if (p.exact_only()) {
         tlo = elo;
         thi = ehi;
     }
     return !(elo > ehi);
 }
 
-// Triangle::intersect decision part (triangle.rs:35-66): returns distance, or -1 on a miss.
-// (A valid hit's distance is a norm, >= 0.)
+// f32 pre-decision of the line slab test on an outward-rounded f32 box.  Returns 1 (the exact
+// f64 test passes), 0 (it fails) or 2 (too close to call: run the exact test).  tlo/thi are
+// conservative: the exact interval lies within [tlo, thi] when 1 is returned.
+// Error bound (DESIGN.md "Traversal"): with |bound|, |origin| <= X (scene extent or |o|), each f32
+// slab value differs from the exact (bound - o)/d by at most ~3e-7 X |1/d_i| + 1.2e-7 |t|
+// (outward box rounding, f32 origin, subtraction, reciprocal and product roundings); E doubles it.
+struct Ray32 {
+    float ox, oy, oz, ix, iy, iz;
+    float ek;  // 6e-7 * X * max_i |1/d_i| (+inf: every test falls back to f64)
+};
+__device__ __forceinline__ Ray32 prepare32(const RayPre& p, double extent) {
+    Ray32 r;
+    r.ox = (float)p.o.x; r.oy = (float)p.o.y; r.oz = (float)p.o.z;
+    r.ix = (float)p.inv.x; r.iy = (float)p.inv.y; r.iz = (float)p.inv.z;
+    // origins on the infinite plane can lie outside the scene extent: bound with |o| too
+    const double big = fmax(extent, fmax(fmax(fabs(p.o.x), fabs(p.o.y)), fabs(p.o.z))) + 1.0;
+    const double m = fmax(fmax(fabs(p.inv.x), fabs(p.inv.y)), fabs(p.inv.z));
+    const double ek = 6e-7 * big * m;
+    r.ek = (p.exact_only() || !(ek < 1e30)) ? INFINITY : (float)ek;
+    return r;
+}
+__device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo, float& thi) {
+    const float ax = (b[0] - r.ox) * r.ix, cx = (b[1] - r.ox) * r.ix;
+    const float ay = (b[2] - r.oy) * r.iy, cy = (b[3] - r.oy) * r.iy;
+    const float az = (b[4] - r.oz) * r.iz, cz = (b[5] - r.oz) * r.iz;
+    const float lo = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fminf(az, cz));
+    const float hi = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fmaxf(az, cz));
+    const float e = r.ek + 2.4e-7f * (fabsf(lo) + fabsf(hi));
+    tlo = lo - e;
+    thi = hi + e;
+    if (hi - lo > 2.0f * e) return 1;
+    if (lo - hi > 2.0f * e) return 0;
+    return 2;
+}
+
+// Triangle::intersect decision part (triangle.rs:35-66): returns distance, or -1 on a miss
+// (a valid hit's distance is a norm, >= 0).  Vertices are translated by -origin (v + (-o) ==
+// v - o bitwise), permuted so the ray's largest signed component is last, sheared (z unscaled).
 __device__ __forceinline__ double triangle_distance(const TriVerts& t, const RayPre& p, double bary[3]) {
-    V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
-    // translate by -origin, permute, shear (z unscaled)
-    double a0x = sel(v0, p.k0) + p.pno.x, a0y = sel(v0, p.k1) + p.pno.y, a0z = sel(v0, p.k2) + p.pno.z;
-    double a1x = sel(v1, p.k0) + p.pno.x, a1y = sel(v1, p.k1) + p.pno.y, a1z = sel(v1, p.k2) + p.pno.z;
-    double a2x = sel(v2, p.k0) + p.pno.x, a2y = sel(v2, p.k1) + p.pno.y, a2z = sel(v2, p.k2) + p.pno.z;
-    double t0x = a0x + p.sx * a0z, t0y = a0y + p.sy * a0z;
-    double t1x = a1x + p.sx * a1z, t1y = a1y + p.sy * a1z;
-    double t2x = a2x + p.sx * a2z, t2y = a2y + p.sy * a2z;
-    // signed_edge_functions (triangle.rs:141-158)
-    double e0 = t1x * t2y - t2x * t1y;
-    double e1 = t2x * t0y - t0x * t2y;
-    double e2 = t0x * t1y - t1x * t0y;
-    bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
+    const int k0 = p.k0(), k1 = p.k1(), k2 = p.k2();
+    const double ox = sel(p.o, k0), oy = sel(p.o, k1), oz = sel(p.o, k2);
+    double tx[3], ty[3], az[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const V3 v = mk(t.v[3 * i], t.v[3 * i + 1], t.v[3 * i + 2]);
+        const double ax = sel(v, k0) + (-ox), ay = sel(v, k1) + (-oy);
+        az[i] = sel(v, k2) + (-oz);
+        tx[i] = ax + p.sx * az[i];
+        ty[i] = ay + p.sy * az[i];
+    }
+    // signed_edge_functions (triangle.rs:141-158): e0 = E(v1, v2), e1 = E(v2, v0), e2 = E(v0, v1)
+    const double e0 = tx[1] * ty[2] - tx[2] * ty[1];
+    const double e1 = tx[2] * ty[0] - tx[0] * ty[2];
+    const double e2 = tx[0] * ty[1] - tx[1] * ty[0];
+    const bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
     if (!((!s0 && !s1 && !s2) || (s0 && s1 && s2))) return -1.0;
-    double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
-    double s = 0.0;
+    const double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
+    double s = 0.0;  // fold(0.0) (triangle.rs:160-162)
     s = s + ea0;
     s = s + ea1;
     s = s + ea2;
-    double inv = 1.0 / s;
-    double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
-    double tz = 0.0;
-    tz = tz + a0z * b0;
-    tz = tz + a1z * b1;
-    tz = tz + a2z * b2;
+    const double inv = 1.0 / s;
+    const double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
+    double tz = 0.0;  // explicit fold(0.0) (triangle.rs:57-61)
+    tz = tz + az[0] * b0;
+    tz = tz + az[1] * b1;
+    tz = tz + az[2] * b2;
     if (sgn(tz) != sgn(p.pdz)) return -1.0;
-    V3 loc = mk(0.0, 0.0, 0.0);
-    loc = add(loc, scl(v0, b0));
-    loc = add(loc, scl(v1, b1));
-    loc = add(loc, scl(v2, b2));
-    V3 dv = sub(p.o, loc);
+    V3 loc = mk(0.0, 0.0, 0.0);  // fold(Vec3::zeros()) (triangle.rs:66-71)
+    loc = add(loc, scl(mk(t.v[0], t.v[1], t.v[2]), b0));
+    loc = add(loc, scl(mk(t.v[3], t.v[4], t.v[5]), b1));
+    loc = add(loc, scl(mk(t.v[6], t.v[7], t.v[8]), b2));
+    const V3 dv = sub(p.o, loc);
     bary[0] = b0;
     bary[1] = b1;
     bary[2] = b2;
@@ -374,6 +413,7 @@ struct Best {
 struct Counts {
     uint32_t box_tests, node_visits, tri_tests, rays, shaded;
     uint32_t trav_slots, outer_slots;  // wave-level loop iterations x 64 (counted by one lane)
+    uint32_t exact_boxes;              // f32 box tests too close to call (f64 fallback)
 };
 __device__ __forceinline__ bool first_active_lane() {
     return __lane_id() == (unsigned)__builtin_ctzll(__ballot(1));
@@ -388,7 +428,7 @@ __device__ __forceinline__ void traverse_bvh(const DeviceScene& S, const Bvh& bv
     auto cull = [&](double tlo, double thi) {
         double bound = best.kind ? best.d : INFINITY;
         if (tlo > bound + margin * (1.0 + fabs(bound))) return true;
-        if (p.behind_ok && thi < -behind) return true;
+        if (p.behind_ok() && thi < -behind) return true;
         return false;
     };
     // triangle candidate: distance ties go to the later leaf within this BVH (closest_intersection

@@ -163,6 +163,7 @@ struct vr_scene {
     std::vector<vr::Prim> prims;
     std::vector<vr::Bvh> bvhs;
     std::vector<vr::Node> nodes;
+    std::vector<vr::Node32> nodes32;
     std::vector<vr::TriVerts> tris;
     std::vector<vr::TriNormals> normals;
     std::vector<std::vector<uint64_t>> leaf_order;  // per mesh
@@ -193,14 +194,16 @@ size_t align_up(size_t v) {
 int upload(vr_scene* s) {
     VR_HIP(hipSetDevice(s->device));
     const size_t sz_nodes = s->nodes.size() * sizeof(vr::Node);
+    const size_t sz_nodes32 = s->nodes32.size() * sizeof(vr::Node32);
     const size_t sz_tris = s->tris.size() * sizeof(vr::TriVerts);
     const size_t sz_norm = s->normals.size() * sizeof(vr::TriNormals);
     const size_t sz_mat = s->materials.size() * sizeof(vr::Material);
     const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
     const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
-    size_t off[7], total = 0;
-    const size_t sizes[7] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh, 64 + 8 * sizeof(unsigned long long)};
-    for (int i = 0; i < 7; ++i) {
+    size_t off[8], total = 0;
+    const size_t sizes[8] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh, 64 + vr::kCntCount * sizeof(unsigned long long),
+                             sz_nodes32};
+    for (int i = 0; i < 8; ++i) {
         off[i] = total;
         total += align_up<char>(std::max<size_t>(sizes[i], 1));
     }
@@ -212,10 +215,12 @@ int upload(vr_scene* s) {
     for (int i = 0; i < 6; ++i)
         if (sizes[i]) VR_HIP(hipMemcpy(base + off[i], src[i], sizes[i], hipMemcpyHostToDevice));
     VR_HIP(hipMemset(base + off[6], 0, sizes[6]));
+    if (sz_nodes32) VR_HIP(hipMemcpy(base + off[7], s->nodes32.data(), sz_nodes32, hipMemcpyHostToDevice));
     s->d_error = (int32_t*)(base + off[6]);
     s->d_counters = (unsigned long long*)(base + off[6] + 64);
     vr::DeviceScene& d = s->dev;
     d.nodes = (const vr::Node*)(base + off[0]);
+    d.nodes32 = (const vr::Node32*)(base + off[7]);
     d.tris = (const vr::TriVerts*)(base + off[1]);
     d.normals = (const vr::TriNormals*)(base + off[2]);
     d.materials = (const vr::Material*)(base + off[3]);
@@ -481,6 +486,26 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     }
     // BVH objects in object order (ties across objects depend on it)
     std::sort(s->bvhs.begin(), s->bvhs.end(), [](const vr::Bvh& a, const vr::Bvh& b) { return a.object < b.object; });
+    // f32 traversal copy: outward rounding keeps each f32 box a superset of its f64 box
+    s->nodes32.resize(s->nodes.size());
+    for (size_t i = 0; i < s->nodes.size(); ++i) {
+        const vr::Node& n = s->nodes[i];
+        vr::Node32& m = s->nodes32[i];
+        std::memset(&m, 0, sizeof m);
+        for (int c = 0; c < 2; ++c) {
+            for (int k = 0; k < 6; ++k) {
+                const double v = n.box[c][k];
+                float f = (float)v;
+                if (k % 2 == 0) {
+                    if ((double)f > v) f = std::nextafter(f, -INFINITY);
+                } else {
+                    if ((double)f < v) f = std::nextafter(f, INFINITY);
+                }
+                m.box[c][k] = f;
+            }
+            m.child[c] = n.child[c];
+        }
+    }
     s->extent = extent;
     vr::DeviceScene& d = s->dev;
     d.prim_count = (int32_t)s->prims.size();
@@ -488,6 +513,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     std::memcpy(d.camera, s->camera, sizeof d.camera);
     d.margin = 1e-9 * (extent + 1.0);
     d.behind_margin = 1e-6 * (extent + 1.0);
+    d.extent = extent;
     if (!s->host_only) {
         int rc = upload(s);
         if (rc != VR_OK) {
@@ -575,6 +601,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
                 stats->samples = c[vr::kCntSamples];
                 stats->traversal_slots = c[vr::kCntTraversalSlots];
                 stats->path_loop_slots = c[vr::kCntOuterSlots];
+                stats->exact_box_tests = c[vr::kCntExactBoxes];
             }
         }
         return read_and_clear_error(s, st);

@@ -25,6 +25,17 @@ struct alignas(128) Node {
 };
 static_assert(sizeof(Node) == 128, "Node must be one 128-B line");
 
+// The traversal copy of a Node: child boxes rounded OUTWARD to f32 (so each f32 box contains
+// its f64 box), same child links, 64 B.  The bunny BVH fits one XCD's 4 MB L2 in this form.
+// A box test is decided from it unless the f32 interval is within its error bound of a tie, in
+// which case the exact f64 box of the same index (Node) is fetched.
+struct alignas(64) Node32 {
+    float box[2][6];   // 48 B
+    int32_t child[2];  //  8 B
+    int32_t pad[2];    //  8 B -> 64 B
+};
+static_assert(sizeof(Node32) == 64, "Node32 must be 64 B");
+
 // Triangle vertices in BVH leaf order, padded to 80 B for 16-B aligned loads.
 struct alignas(16) TriVerts {
     double v[9];
@@ -70,6 +81,7 @@ struct Bvh {
 // Device view of a scene (all pointers are device pointers on one GPU).
 struct DeviceScene {
     const Node* nodes;
+    const Node32* nodes32;
     const TriVerts* tris;
     const TriNormals* normals;
     const Material* materials;
@@ -80,6 +92,7 @@ struct DeviceScene {
     double camera[3];
     double margin;         // distance-cull slack (absolute + relative), see DESIGN.md "Traversal"
     double behind_margin;  // cull of boxes entirely behind the origin
+    double extent;         // max |coordinate| of camera and geometry (f32 box-test error bound)
 };
 
 struct RenderArgs {
@@ -115,7 +128,8 @@ enum Counter : int {
     kCntSamples = 5,
     kCntTraversalSlots = 6,  // 64 x wave-level traversal-loop iterations (lane-slot occupancy)
     kCntOuterSlots = 7,      // 64 x wave-level path-loop iterations
-    kCntCount = 8
+    kCntExactBoxes = 8,      // f32 box tests that fell back to the exact f64 test
+    kCntCount = 16
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).

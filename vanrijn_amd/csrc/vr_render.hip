@@ -38,249 +38,37 @@ namespace dev {
 // ----------------------------------------------------------------------------------------------
 __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}; }  // mod.rs:41-46
 
-template <int STACK, bool COUNT, bool RECORD, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void render_kernel_v1(RenderArgs A) {
-    __shared__ int st_node[STACK * 256];
-    __shared__ float st_t[STACK * 256];
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    // 16x16 pixel block per workgroup, 8x8 per wave
-    const uint64_t bx = blockIdx.x % ((A.tile_width + 15) / 16);
-    const uint64_t by = blockIdx.x / ((A.tile_width + 15) / 16);
-    const uint64_t px = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint64_t py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool live = px < A.tile_width && py < A.tile_height;
-    const DeviceScene& S = A.scene;
-    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t samples_done = 0;
-
-    const uint64_t row = A.start_row + py, col = A.start_column + px;
-    const uint64_t pix = py * A.tile_width + px;
-    // Kahan state (accumulation_buffer.rs:44-60)
-    double sum0 = 0.0, sum1 = 0.0, sum2 = 0.0, bias0 = 0.0, bias1 = 0.0, bias2 = 0.0, wsum = 0.0, wbias = 0.0;
-    if (live && A.accumulate) {
-        const double* s = A.state + pix * 8;
-        sum0 = s[0]; sum1 = s[1]; sum2 = s[2]; bias0 = s[3]; bias1 = s[4]; bias2 = s[5]; wsum = s[6]; wbias = s[7];
-    }
-    // camera (camera.rs:24-43)
-    const double fw_d = (double)A.width, fh_d = (double)A.height;
-    double film_w, film_h;
-    if (fw_d > fh_d) { film_w = fw_d / fh_d; film_h = 1.0; } else { film_w = 1.0; film_h = fw_d / fh_d; }
-    const double pixel_w = film_w * (1.0 / fw_d), pixel_h = film_h * (1.0 / fh_d);
-    const V3 cam = mk(S.camera[0], S.camera[1], S.camera[2]);
-
-    uint32_t s_idx = 0;
-    bool need_camera = true;
-    bool active = live && A.spp > 0;
-    Rng rng;
-    Ray ray;
-    int depth = -1;     // -1: tracing the camera ray; k >= 0: tracing level k's bounce ray
-    double lambda = 0.0;
-    double T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0;  // forward throughput at lambda and at 0
-    V3 wo_world = mk(0.0, 0.0, 0.0);
-    int bounces = 0, flags = 0;
-
-    auto finish = [&](double wl, double I) {
-        // update_pixel(row, column, photon.scale_intensity(360), 1.0)
-        double Is = I * 360.0;
-        V3 c = xyz_for_wavelength(wl);
-        double cx = c.x * Is, cy = c.y * Is, cz = c.z * Is;
-        double wy = 1.0 - wbias;
-        double wt = wsum + wy;
-        wbias = (wt - wsum) - wy;
-        wsum = wt;
-        { double y = cx * 1.0 - bias0; double t = sum0 + y; bias0 = (t - sum0) - y; sum0 = t; }
-        { double y = cy * 1.0 - bias1; double t = sum1 + y; bias1 = (t - sum1) - y; sum1 = t; }
-        { double y = cz * 1.0 - bias2; double t = sum2 + y; bias2 = (t - sum2) - y; sum2 = t; }
-        if (RECORD) {
-            vr_sample_record* rec = (vr_sample_record*)A.records + (pix * A.spp + s_idx);
-            rec->wavelength = wl;
-            rec->intensity = I;
-            rec->xyz[0] = cx;
-            rec->xyz[1] = cy;
-            rec->xyz[2] = cz;
-            rec->bounces = bounces;
-            rec->flags = flags;
-        }
-        if (COUNT) samples_done++;
-        ++s_idx;
-        need_camera = true;
-    };
-
-    while (active) {
-        if (COUNT && first_active_lane()) cnt.outer_slots += 64;
-        if (need_camera) {
-            if (s_idx == A.spp) { active = false; break; }
-            rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
-            rng.k = 0;
-            // ImageSampler::ray_for_pixel (camera.rs:52-66): x's draw first
-            double ux = rng.standard();
-            double uy = rng.standard();
-            double x = ((double)col + ux) * pixel_w - film_w * 0.5;
-            double y = ((double)(A.height - (row + 1)) + uy) * pixel_h - film_h * 0.5;
-            ray = ray_new(cam, mk(x, y, 1.0));
-            depth = -1;
-            bounces = 0;
-            flags = 0;
-            need_camera = false;
-        }
-        RayPre pre = prepare(ray);
-        Best best = closest_hit<STACK, COUNT>(S, pre, st_node, st_t, tid, cnt);
-        if (depth < 0) {
-            if (!best.kind) { finish(0.0, 0.0); continue; }  // camera.rs:110-113
-            flags |= 1;
-            lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
-            T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0;
-            depth = 0;
-        } else {
-            if (!best.kind) {  // sky (simple_random_integrator.rs:43-46)
-                double L = sky_intensity(wo_world.y, lambda);
-                finish(lambda, Acc + T * L);
-                continue;
-            }
-            depth += 1;
-            if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
-                flags |= 2;
-                finish(0.0, Acc0);
-                continue;
-            }
-        }
-        // ---- shade level `depth` (simple_random_integrator.rs:20-53)
-        HitInfo h;
-        hit_info(S, best, pre, h);
-        if (COUNT && best.kind == kTri) cnt.shaded++;
-        // world_to_bsdf = rows(tangent, cotangent, normal); bsdf_to_world = cofactor^T * det
-        const double m00 = h.tangent.x, m01 = h.tangent.y, m02 = h.tangent.z;
-        const double m10 = h.cotangent.x, m11 = h.cotangent.y, m12 = h.cotangent.z;
-        const double m20 = h.normal.x, m21 = h.normal.y, m22 = h.normal.z;
-        const double mi00 = m11 * m22 - m12 * m21, mi01 = m10 * m22 - m12 * m20, mi02 = m10 * m21 - m11 * m20;
-        const double mi10 = m01 * m22 - m02 * m21, mi11 = m00 * m22 - m02 * m20, mi12 = m00 * m21 - m01 * m20;
-        const double mi20 = m01 * m12 - m02 * m11, mi21 = m00 * m12 - m02 * m10, mi22 = m00 * m11 - m01 * m10;
-        const double det = m00 * mi00 - m01 * mi01 + m02 * mi02;
-        if (det == 0.0) {  // the reference panics ("Expected matrix to be invertable.")
-            flags |= 4;
-            atomicOr(A.error_flag, 1);
-            finish(0.0, 0.0);
-            continue;
-        }
-        // inverse[i][j] = cofactor(j, i) * det, cofactor(r, c) = (-1)^(r+c) * minor(r, c)
-        const V3 inv0 = mk((1.0 * mi00) * det, (-1.0 * mi10) * det, (1.0 * mi20) * det);
-        const V3 inv1 = mk((-1.0 * mi01) * det, (1.0 * mi11) * det, (-1.0 * mi21) * det);
-        const V3 inv2 = mk((1.0 * mi02) * det, (-1.0 * mi12) * det, (1.0 * mi22) * det);
-        const V3 w_i = mk(dot(h.tangent, h.retro), dot(h.cotangent, h.retro), dot(h.normal, h.retro));
-        const Material* mat = &S.materials[h.material];
-        V3 w_o;
-        double pdf;
-        if (mat->kind == 1) {  // reflective_material.rs:42-47
-            w_o = mk(-w_i.x, -w_i.y, w_i.z);
-            pdf = 1.0;
-        } else {  // lambertian_material.rs:36-59: rejection sampling on Open01 pairs
-            double x = 2.0 * rng.open01() - 1.0;
-            double y = 2.0 * rng.open01() - 1.0;
-            while (dot(mk(x, y, 0.0), mk(x, y, 0.0)) > 1.0) {
-                x = 2.0 * rng.open01() - 1.0;
-                y = 2.0 * rng.open01() - 1.0;
-            }
-            double z = fmax(sqrt(1.0 - x * x - y * y), 0.0);
-            V3 w = mk(x, y, z);
-            double cos_theta = dot(w, mk(0.0, 0.0, 1.0));
-            double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-            w_o = normalize(w);
-            pdf = (cos_theta * sin_theta) / 3.14159265358979323846;
-        }
-        wo_world = mk(dot(inv0, w_o), dot(inv1, w_o), dot(inv2, w_o));
-        const double cosf = fabs(dot(wo_world, h.normal));
-        // bsdf() applied to photon.scale_intensity(pdf).scale_intensity(|cos|), forward form
-        double a, a0, bterm;
-        const double c_l = material_colour(mat, lambda);
-        const double c_0 = material_colour(mat, 0.0);
-        if (mat->kind == 1) {  // reflective_material.rs:17-39
-            if (w_i.z <= 0.0 || w_o.z <= 0.0) {
-                a = 0.0; a0 = 0.0; bterm = 0.0;
-            } else {
-                V3 refl = mk(-w_o.x, -w_o.y, w_o.z);
-                double cth = dot(w_i, refl);
-                cth = cth < 0.0 ? 0.0 : (cth > 1.0 ? 1.0 : cth);
-                double theta = acos(fabs(cth));
-                const double sigma = 0.05, two = 2.0;
-                double f = mat->reflection * exp(-(pow(theta, two)) / (two * sigma * sigma));
-                a = (((pdf * cosf) * c_l) * mat->diffuse) * (1.0 - f);
-                a0 = (((pdf * cosf) * c_0) * mat->diffuse) * (1.0 - f);
-                bterm = f;
-            }
-        } else {  // lambertian_material.rs:27-34
-            a = ((pdf * cosf) * c_l) * mat->diffuse;
-            a0 = ((pdf * cosf) * c_0) * mat->diffuse;
-            bterm = 0.0;
-        }
-        Acc = Acc + T * bterm;
-        T = T * a;
-        Acc0 = Acc0 + T0 * bterm;
-        T0 = T0 * a0;
-        if (!RECORD && T == 0.0 && Acc == 0.0 && T0 == 0.0 && Acc0 == 0.0) {
-            // every continuation of this path yields intensity 0 (sky or recursion limit): the
-            // sample's colour is 0 whatever is traced next
-            finish(lambda, 0.0);
-            continue;
-        }
-        // Ray::new(location, w_o).bias(1e-7): normalise, step, normalise again (mod.rs:41-61)
-        Ray r0 = ray_new(h.loc, wo_world);
-        ray = ray_new(add(r0.o, scl(r0.d, kBounceBias)), r0.d);
-        ++bounces;
-    }
-
-    if (live) {
-        double* s = A.state + pix * 8;
-        s[0] = sum0; s[1] = sum1; s[2] = sum2; s[3] = bias0; s[4] = bias1; s[5] = bias2; s[6] = wsum; s[7] = wbias;
-    }
-    if (COUNT) {
-        atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
-        atomicAdd(&A.counters[kCntNodeVisits], (unsigned long long)cnt.node_visits);
-        atomicAdd(&A.counters[kCntTriangleTests], (unsigned long long)cnt.tri_tests);
-        atomicAdd(&A.counters[kCntRays], (unsigned long long)cnt.rays);
-        atomicAdd(&A.counters[kCntShadedTriangles], (unsigned long long)cnt.shaded);
-        atomicAdd(&A.counters[kCntSamples], (unsigned long long)samples_done);
-        atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
-        atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
-    }
-}
-
 // ----------------------------------------------------------------------------------------------
-// Render kernel v2: one pixel per lane, traversal and shading interleaved by phases.
+// Render kernel: one pixel per lane, traversal and shading interleaved by phases.
 //
-// v1 (render_kernel_v1) traces one ray per lane per path-loop iteration, so a wave's traversal
-// loop runs as long as its longest ray (measured lane utilisation 25 %).  v2 keeps each lane's
-// traversal state (node, LDS stack, closest hit so far) alive across iterations: the wave steps
-// nodes for all traversing lanes until at least `shade_threshold` lanes have finished, then those
-// lanes shade (BSDF, next bounce ray or sample end + next camera ray) and rejoin the traversal
-// while the unfinished lanes resume where they stopped.  Kahan sums live in LDS, the stack holds
-// node indices only (a popped subtree is culled by its children's box tests), which keeps the
-// kernel at 4 workgroups (16 waves) per CU.
+// A first version traced one ray per lane per path-loop iteration, so a wave's traversal loop ran
+// as long as its longest ray (measured lane utilisation 25 %).  Here each lane's traversal state
+// (node, LDS stack, closest hit so far) stays alive across iterations: the wave steps BVH nodes
+// for all traversing lanes until at least `shade_threshold` lanes have finished, then those lanes
+// shade (BSDF, next bounce ray -- or the sample's end and the next sample's camera ray) and
+// rejoin the traversal while unfinished lanes resume where they stopped.  Kahan sums live in LDS
+// and the stack holds node indices only (a popped subtree is culled by its children's box tests).
 // ----------------------------------------------------------------------------------------------
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
 
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MINW = 1>
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MINW = 3>
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ uint32_t st_node[STACK * 256];
     __shared__ double kahan[8 * 256];  // [sum x, sum y, sum z, bias x, bias y, bias z, weight, weight_bias][tid]
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint64_t bx = blockIdx.x % ((A.tile_width + 15) / 16);
-    const uint64_t by = blockIdx.x / ((A.tile_width + 15) / 16);
-    const uint64_t px = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint64_t py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool live = px < A.tile_width && py < A.tile_height;
     const DeviceScene& S = A.scene;
-    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t px, py;
+    {
+        const int wave = tid >> 6, lane = tid & 63;
+        const uint32_t bw = (uint32_t)((A.tile_width + 15) / 16);
+        px = (blockIdx.x % bw) * 16 + (wave & 1) * 8 + (lane & 7);
+        py = (blockIdx.x / bw) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    }
+    const bool live = px < A.tile_width && py < A.tile_height;
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t samples_done = 0;
-    const uint64_t row = A.start_row + py, col = A.start_column + px;
-    const uint64_t pix = py * A.tile_width + px;
-    for (int k = 0; k < 8; ++k) kahan[k * 256 + tid] = (live && A.accumulate) ? A.state[pix * 8 + k] : 0.0;
-
-    const double fw_d = (double)A.width, fh_d = (double)A.height;
-    double film_w, film_h;
-    if (fw_d > fh_d) { film_w = fw_d / fh_d; film_h = 1.0; } else { film_w = 1.0; film_h = fw_d / fh_d; }
-    const double pixel_w = film_w * (1.0 / fw_d), pixel_h = film_h * (1.0 / fh_d);
+    for (int k = 0; k < 8; ++k)
+        kahan[k * 256 + tid] = (live && A.accumulate) ? A.state[((uint64_t)py * A.tile_width + px) * 8 + k] : 0.0;
 
     int state = (live && A.spp > 0) ? kNeedRay : kDone;
     uint32_t s_idx = 0;
@@ -288,22 +76,22 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     rng.base = 0;
     rng.k = 0;
     RayPre pre;
+    Ray32 pre32;
     Best best;
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
 
-    // the BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
+    // BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
     auto culled = [&](double tlo, double thi) {
-        double bound = best.kind ? best.d : INFINITY;
+        const double bound = best.kind ? best.d : INFINITY;
         if (tlo > bound + S.margin * (1.0 + fabs(bound))) return true;
-        if (pre.behind_ok && thi < -S.behind_margin) return true;
-        return false;
+        return pre.behind_ok() && thi < -S.behind_margin;
     };
     auto test_tri = [&](int tri) {
         if (COUNT) cnt.tri_tests++;
         double b[3];
-        double d = triangle_distance(S.tris[tri], pre, b);
+        const double d = triangle_distance(S.tris[tri], pre, b);
         if (d < 0.0) return;
         bool take;
         if (!best.kind || d < best.d) take = true;
@@ -316,7 +104,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             best.object = cur_object;
         }
     };
-    // find the next BVH (from bvh_i) with work: returns false when the ray is fully traced
+    // next BVH (from bvh_i) with work; false when the ray is fully traced
     auto start_bvhs = [&]() {
         for (; bvh_i < S.bvh_count; ++bvh_i) {
             const Bvh& bvh = S.bvhs[bvh_i];
@@ -335,9 +123,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         }
         return false;
     };
-    // a new ray: analytic primitives first (object then position order), then the BVHs
+    // a new ray (directions already normalised): primitive lists first, then the BVHs
     auto begin_ray = [&](V3 o, V3 d) {
         pre = prepare(Ray{o, d});
+        pre32 = prepare32(pre, S.extent);
         if (COUNT) cnt.rays++;
         best.kind = kNone;
         best.d = 0.0;
@@ -349,7 +138,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             bool ok;
             if (pr.kind == 0) ok = plane_distance(pr, pre, dd);
             else { dd = sphere_distance(pr, pre); ok = dd >= 0.0; }
-            if (ok && (!best.kind || dd < best.d)) {
+            if (ok && (!best.kind || dd < best.d)) {  // min_by keeps the first of equals
                 best.d = dd;
                 best.kind = kPrim;
                 best.index = i;
@@ -361,31 +150,31 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         state = start_bvhs() ? kTraversing : kTraversed;
     };
     auto finish = [&](double wl, double I) {  // update_pixel(row, col, photon x 360, 1.0)
-        double Is = I * 360.0;
-        V3 c = xyz_for_wavelength(wl);
-        double cx = c.x * Is, cy = c.y * Is, cz = c.z * Is;
+        const double Is = I * 360.0;
+        const V3 c = xyz_for_wavelength(wl);
+        const double cc[3] = {c.x * Is, c.y * Is, c.z * Is};
         double* K = kahan + tid;
-        double wsum = K[6 * 256], wbias = K[7 * 256];
-        double wy = 1.0 - wbias;
-        double wt = wsum + wy;
+        const double wsum = K[6 * 256], wbias = K[7 * 256];
+        const double wy = 1.0 - wbias;
+        const double wt = wsum + wy;
         K[7 * 256] = (wt - wsum) - wy;
         K[6 * 256] = wt;
-        const double cc[3] = {cx, cy, cz};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            double sum = K[k * 256], bias = K[(3 + k) * 256];
-            double y = cc[k] * 1.0 - bias;
-            double t = sum + y;
+            const double sum = K[k * 256], bias = K[(3 + k) * 256];
+            const double y = cc[k] * 1.0 - bias;
+            const double t = sum + y;
             K[(3 + k) * 256] = (t - sum) - y;
             K[k * 256] = t;
         }
         if (RECORD) {
-            vr_sample_record* rec = (vr_sample_record*)A.records + (pix * A.spp + s_idx);
+            vr_sample_record* rec =
+                (vr_sample_record*)A.records + (((uint64_t)py * A.tile_width + px) * A.spp + s_idx);
             rec->wavelength = wl;
             rec->intensity = I;
-            rec->xyz[0] = cx;
-            rec->xyz[1] = cy;
-            rec->xyz[2] = cz;
+            rec->xyz[0] = cc[0];
+            rec->xyz[1] = cc[1];
+            rec->xyz[2] = cc[2];
             rec->bounces = bounces;
             rec->flags = flags;
         }
@@ -393,21 +182,115 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         ++s_idx;
         state = kNeedRay;
     };
+    // one level of SimpleRandomIntegrator::integrate (simple_random_integrator.rs:20-53) at the
+    // closest hit, forward form: returns true when a bounce ray was started
+    auto shade = [&]() {
+        HitInfo h;
+        hit_info(S, best, pre, h);
+        if (COUNT && best.kind == kTri) cnt.shaded++;
+        // world_to_bsdf = rows(tangent, cotangent, normal) (algebra_utils.rs:3-5); its
+        // determinant via the first-row minors (mat3.rs:106-109)
+        const double det = h.tangent.x * (h.cotangent.y * h.normal.z - h.cotangent.z * h.normal.y) -
+                           h.tangent.y * (h.cotangent.x * h.normal.z - h.cotangent.z * h.normal.x) +
+                           h.tangent.z * (h.cotangent.x * h.normal.y - h.cotangent.y * h.normal.x);
+        if (det == 0.0) {  // try_inverse() == None: the reference panics ("Expected matrix to be invertable.")
+            flags |= 4;
+            atomicOr(A.error_flag, 1);
+            finish(0.0, 0.0);
+            return;
+        }
+        const V3 w_i = mk(dot(h.tangent, h.retro), dot(h.cotangent, h.retro), dot(h.normal, h.retro));
+        const Material* mat = &S.materials[h.material];
+        V3 w_o;
+        double pdf;
+        if (mat->kind == 1) {  // reflective_material.rs:42-47
+            w_o = mk(-w_i.x, -w_i.y, w_i.z);
+            pdf = 1.0;
+        } else {  // lambertian_material.rs:36-59: rejection sampling on Open01 pairs
+            double x = 2.0 * rng.open01() - 1.0;
+            double y = 2.0 * rng.open01() - 1.0;
+            while (dot(mk(x, y, 0.0), mk(x, y, 0.0)) > 1.0) {
+                x = 2.0 * rng.open01() - 1.0;
+                y = 2.0 * rng.open01() - 1.0;
+            }
+            const double z = fmax(sqrt(1.0 - x * x - y * y), 0.0);
+            const V3 w = mk(x, y, z);
+            const double cos_theta = dot(w, mk(0.0, 0.0, 1.0));
+            const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+            w_o = normalize(w);
+            pdf = (cos_theta * sin_theta) / 3.14159265358979323846;
+        }
+        // bsdf_to_world = cofactor(M)^T * det (mat3.rs:111-118), applied to w_o by rows
+        V3 wo_world;
+        {
+            const double m00 = h.tangent.x, m01 = h.tangent.y, m02 = h.tangent.z;
+            const double m10 = h.cotangent.x, m11 = h.cotangent.y, m12 = h.cotangent.z;
+            const double m20 = h.normal.x, m21 = h.normal.y, m22 = h.normal.z;
+            const V3 inv0 = mk((1.0 * (m11 * m22 - m12 * m21)) * det, (-1.0 * (m01 * m22 - m02 * m21)) * det,
+                               (1.0 * (m01 * m12 - m02 * m11)) * det);
+            wo_world.x = dot(inv0, w_o);
+            const V3 inv1 = mk((-1.0 * (m10 * m22 - m12 * m20)) * det, (1.0 * (m00 * m22 - m02 * m20)) * det,
+                               (-1.0 * (m00 * m12 - m02 * m10)) * det);
+            wo_world.y = dot(inv1, w_o);
+            const V3 inv2 = mk((1.0 * (m10 * m21 - m11 * m20)) * det, (-1.0 * (m00 * m21 - m01 * m20)) * det,
+                               (1.0 * (m00 * m11 - m01 * m10)) * det);
+            wo_world.z = dot(inv2, w_o);
+        }
+        const double cosf = fabs(dot(wo_world, h.normal));
+        const double c_l = material_colour(mat, lambda);
+        const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
+        double a, a0, bterm;
+        if (mat->kind == 1) {  // reflective_material.rs:17-39
+            if (w_i.z <= 0.0 || w_o.z <= 0.0) {
+                a = 0.0; a0 = 0.0; bterm = 0.0;
+            } else {
+                const V3 refl = mk(-w_o.x, -w_o.y, w_o.z);
+                double cth = dot(w_i, refl);
+                cth = cth < 0.0 ? 0.0 : (cth > 1.0 ? 1.0 : cth);
+                const double theta = acos(fabs(cth));
+                const double sigma = 0.05, two = 2.0;
+                const double f = mat->reflection * exp(-(pow(theta, two)) / (two * sigma * sigma));
+                a = (((pdf * cosf) * c_l) * mat->diffuse) * (1.0 - f);
+                a0 = (((pdf * cosf) * c_0) * mat->diffuse) * (1.0 - f);
+                bterm = f;
+            }
+        } else {  // lambertian_material.rs:27-34
+            a = ((pdf * cosf) * c_l) * mat->diffuse;
+            a0 = ((pdf * cosf) * c_0) * mat->diffuse;
+            bterm = 0.0;
+        }
+        if (depth == 0) b0 = bterm;
+        Acc = Acc + T * bterm;
+        T = T * a;
+        if (!DARK0) {
+            Acc0 = Acc0 + T0 * bterm;
+            T0 = T0 * a0;
+        }
+        const bool zero_tail = DARK0 ? (b0 == 0.0) : (T0 == 0.0 && Acc0 == 0.0);
+        if (!RECORD && T == 0.0 && Acc == 0.0 && zero_tail) {
+            finish(lambda, 0.0);  // every continuation yields intensity 0
+            return;
+        }
+        // Ray::new(location, w_o).bias(1e-7): normalise, step, normalise again (mod.rs:41-61)
+        wo_y = wo_world.y;
+        const V3 d1 = normalize(wo_world);
+        ++bounces;
+        begin_ray(add(h.loc, scl(d1, kBounceBias)), normalize(d1));
+    };
 
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
         if (COUNT && first_active_lane()) cnt.outer_slots += 64;
         if (state == kTraversed) {
-            bool shade = false;
             if (depth < 0) {
                 if (!best.kind) {
-                    finish(0.0, 0.0);  // camera.rs:110-113
+                    finish(0.0, 0.0);  // camera ray missed: photon {0, 0} (camera.rs:110-113)
                 } else {
                     flags |= 1;
                     lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
                     T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0; b0 = 0.0;
                     depth = 0;
-                    shade = true;
+                    shade();
                 }
             } else if (!best.kind) {
                 finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
@@ -417,91 +300,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                     flags |= 2;
                     finish(0.0, DARK0 ? b0 : Acc0);
                 } else {
-                    shade = true;
-                }
-            }
-            if (shade) {
-                HitInfo h;
-                hit_info(S, best, pre, h);
-                if (COUNT && best.kind == kTri) cnt.shaded++;
-                const double m00 = h.tangent.x, m01 = h.tangent.y, m02 = h.tangent.z;
-                const double m10 = h.cotangent.x, m11 = h.cotangent.y, m12 = h.cotangent.z;
-                const double m20 = h.normal.x, m21 = h.normal.y, m22 = h.normal.z;
-                const double mi00 = m11 * m22 - m12 * m21, mi01 = m10 * m22 - m12 * m20, mi02 = m10 * m21 - m11 * m20;
-                const double mi10 = m01 * m22 - m02 * m21, mi11 = m00 * m22 - m02 * m20, mi12 = m00 * m21 - m01 * m20;
-                const double mi20 = m01 * m12 - m02 * m11, mi21 = m00 * m12 - m02 * m10, mi22 = m00 * m11 - m01 * m10;
-                const double det = m00 * mi00 - m01 * mi01 + m02 * mi02;
-                if (det == 0.0) {  // the reference panics ("Expected matrix to be invertable.")
-                    flags |= 4;
-                    atomicOr(A.error_flag, 1);
-                    finish(0.0, 0.0);
-                } else {
-                    const V3 w_i = mk(dot(h.tangent, h.retro), dot(h.cotangent, h.retro), dot(h.normal, h.retro));
-                    const Material* mat = &S.materials[h.material];
-                    V3 w_o;
-                    double pdf;
-                    if (mat->kind == 1) {  // reflective_material.rs:42-47
-                        w_o = mk(-w_i.x, -w_i.y, w_i.z);
-                        pdf = 1.0;
-                    } else {  // lambertian_material.rs:36-59
-                        double x = 2.0 * rng.open01() - 1.0;
-                        double y = 2.0 * rng.open01() - 1.0;
-                        while (dot(mk(x, y, 0.0), mk(x, y, 0.0)) > 1.0) {
-                            x = 2.0 * rng.open01() - 1.0;
-                            y = 2.0 * rng.open01() - 1.0;
-                        }
-                        double z = fmax(sqrt(1.0 - x * x - y * y), 0.0);
-                        V3 w = mk(x, y, z);
-                        double cos_theta = dot(w, mk(0.0, 0.0, 1.0));
-                        double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-                        w_o = normalize(w);
-                        pdf = (cos_theta * sin_theta) / 3.14159265358979323846;
-                    }
-                    // bsdf_to_world = cofactor^T * det (mat3.rs:111-118)
-                    const V3 inv0 = mk((1.0 * mi00) * det, (-1.0 * mi10) * det, (1.0 * mi20) * det);
-                    const V3 inv1 = mk((-1.0 * mi01) * det, (1.0 * mi11) * det, (-1.0 * mi21) * det);
-                    const V3 inv2 = mk((1.0 * mi02) * det, (-1.0 * mi12) * det, (1.0 * mi22) * det);
-                    const V3 wo_world = mk(dot(inv0, w_o), dot(inv1, w_o), dot(inv2, w_o));
-                    const double cosf = fabs(dot(wo_world, h.normal));
-                    const double c_l = material_colour(mat, lambda);
-                    const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
-                    double a, a0, bterm;
-                    if (mat->kind == 1) {  // reflective_material.rs:17-39
-                        if (w_i.z <= 0.0 || w_o.z <= 0.0) {
-                            a = 0.0; a0 = 0.0; bterm = 0.0;
-                        } else {
-                            V3 refl = mk(-w_o.x, -w_o.y, w_o.z);
-                            double cth = dot(w_i, refl);
-                            cth = cth < 0.0 ? 0.0 : (cth > 1.0 ? 1.0 : cth);
-                            double theta = acos(fabs(cth));
-                            const double sigma = 0.05, two = 2.0;
-                            double f = mat->reflection * exp(-(pow(theta, two)) / (two * sigma * sigma));
-                            a = (((pdf * cosf) * c_l) * mat->diffuse) * (1.0 - f);
-                            a0 = (((pdf * cosf) * c_0) * mat->diffuse) * (1.0 - f);
-                            bterm = f;
-                        }
-                    } else {  // lambertian_material.rs:27-34
-                        a = ((pdf * cosf) * c_l) * mat->diffuse;
-                        a0 = ((pdf * cosf) * c_0) * mat->diffuse;
-                        bterm = 0.0;
-                    }
-                    if (depth == 0) b0 = bterm;
-                    Acc = Acc + T * bterm;
-                    T = T * a;
-                    if (!DARK0) {
-                        Acc0 = Acc0 + T0 * bterm;
-                        T0 = T0 * a0;
-                    }
-                    const bool zero_tail = DARK0 ? (b0 == 0.0) : (T0 == 0.0 && Acc0 == 0.0);
-                    if (!RECORD && T == 0.0 && Acc == 0.0 && zero_tail) {
-                        finish(lambda, 0.0);  // every continuation yields intensity 0
-                    } else {
-                        // Ray::new(location, w_o).bias(1e-7) (mod.rs:41-61)
-                        wo_y = wo_world.y;
-                        V3 d1 = normalize(wo_world);
-                        ++bounces;
-                        begin_ray(add(h.loc, scl(d1, kBounceBias)), normalize(d1));
-                    }
+                    shade();
                 }
             }
         }
@@ -509,12 +308,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             if (s_idx == A.spp) {
                 state = kDone;
             } else {
+                const uint64_t row = A.start_row + py, col = A.start_column + px;
                 rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
                 rng.k = 0;
-                double ux = rng.standard();  // camera.rs:52-66: x's draw first
-                double uy = rng.standard();
-                double x = ((double)col + ux) * pixel_w - film_w * 0.5;
-                double y = ((double)(A.height - (row + 1)) + uy) * pixel_h - film_h * 0.5;
+                // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
+                const double fw_d = (double)A.width, fh_d = (double)A.height;
+                const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
+                const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
+                const double ux = rng.standard();
+                const double uy = rng.standard();
+                const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
+                const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
                 depth = -1;
                 bounces = 0;
                 flags = 0;
@@ -526,20 +330,25 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         do {
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             if (state == kTraversing) {
-                const Node& nd = S.nodes[node];
+                const Node32& nd = S.nodes32[node];
                 if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
-                double lo0, hi0, lo1, hi1;
                 const int c0 = nd.child[0], c1 = nd.child[1];
-                bool h0 = slab(nd.box[0], pre, lo0, hi0) && !culled(lo0, hi0);
-                bool h1 = slab(nd.box[1], pre, lo1, hi1) && !culled(lo1, hi1);
+                float f0, g0, f1, g1;
+                const int r0 = slab32(nd.box[0], pre32, f0, g0);
+                const int r1 = slab32(nd.box[1], pre32, f1, g1);
+                double lo0 = f0, hi0 = g0, lo1 = f1, hi1 = g1;
+                bool h0 = r0 == 1, h1 = r1 == 1;
+                if (r0 == 2) { if (COUNT) cnt.exact_boxes++; h0 = slab(S.nodes[node].box[0], pre, lo0, hi0); }
+                if (r1 == 2) { if (COUNT) cnt.exact_boxes++; h1 = slab(S.nodes[node].box[1], pre, lo1, hi1); }
+                h0 = h0 && !culled(lo0, hi0);
+                h1 = h1 && !culled(lo1, hi1);
                 if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
                 if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
                 if (h0 && h1) {
-                    int near = c0, far = c1;
-                    if (lo1 < lo0) { near = c1; far = c0; }
-                    st_node[sp * 256 + tid] = (uint32_t)far;
+                    const bool swap = lo1 < lo0;  // near child first
+                    st_node[sp * 256 + tid] = (uint32_t)(swap ? c0 : c1);
                     ++sp;
-                    node = near;
+                    node = swap ? c1 : c0;
                 } else if (h0) {
                     node = c0;
                 } else if (h1) {
@@ -557,7 +366,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     }
 
     if (live)
-        for (int k = 0; k < 8; ++k) A.state[pix * 8 + k] = kahan[k * 256 + tid];
+        for (int k = 0; k < 8; ++k) A.state[((uint64_t)py * A.tile_width + px) * 8 + k] = kahan[k * 256 + tid];
     if (COUNT) {
         atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
         atomicAdd(&A.counters[kCntNodeVisits], (unsigned long long)cnt.node_visits);
@@ -567,6 +376,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         atomicAdd(&A.counters[kCntSamples], (unsigned long long)samples_done);
         atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
         atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
+        atomicAdd(&A.counters[kCntExactBoxes], (unsigned long long)cnt.exact_boxes);
     }
 }
 
@@ -581,7 +391,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
     r.o = ldv(A.origins + 3 * i);
     r.d = ldv(A.directions + 3 * i);
     RayPre pre = prepare(r);
-    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     Best best = closest_hit<STACK, false>(A.scene, pre, st_node, st_t, tid, cnt);
     vr_hit_record* out = (vr_hit_record*)A.out + i;
     out->valid = best.kind != kNone;
@@ -611,15 +421,12 @@ template <int STACK>
 static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, hipStream_t s) {
     const uint64_t blocks = ((a.tile_width + 15) / 16) * ((a.tile_height + 15) / 16);
     dim3 grid((unsigned)blocks), block(256);
-    // experiment hook (tools/variants.py): 1 = v1 kernel, 2/3/4 = v2 with that many waves per SIMD
+    // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3:
+    // measured fastest, 168 VGPRs with a few cold spills; 2 and 4 are 15-20 % and 8 % slower)
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
-    if (variant == 1 && !recording) {
-        if (counting) hipLaunchKernelGGL((dev::render_kernel_v1<STACK, true, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((dev::render_kernel_v1<STACK, false, false>), grid, block, 0, s, a);
-        return hipGetLastError();
-    }
-    if (variant >= 2 && variant <= 4 && !recording && !counting && dark0) {
+    if (variant >= 1 && variant <= 4 && variant != 3 && !recording && !counting && dark0) {
+        if (variant == 1) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 1>), grid, block, 0, s, a);
         if (variant == 2) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 2>), grid, block, 0, s, a);
         if (variant == 3) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3>), grid, block, 0, s, a);
         if (variant == 4) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 4>), grid, block, 0, s, a);
