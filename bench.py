@@ -54,6 +54,24 @@ def algorithmic_bytes(c, pixels):
             BYTES_PER_PIXEL_STATE * pixels)
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc.sh +
+    tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE), used only when it was collected on this
+    exact library build and bench configuration; otherwise None."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    lib = os.path.join(ROOT, "vanrijn_amd", "lib", "libvanrijn_amd.so")
+    try:
+        rec = json.load(open(path))
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    except (OSError, ValueError):
+        return None
+    want = f"--width {args.width} --height {args.height} --spp {args.spp} --scene {args.scene}"
+    if rec.get("lib_sha256") != sha or rec.get("config") != want:
+        return None
+    return rec.get("hbm_bytes_per_launch")
+
+
 def cpu_baseline(scene, width, height, seconds, threads):
     """Oracle (reference mode) on the host: full frame, first k sample indices, k chosen so the
     run takes about `seconds`."""
@@ -162,7 +180,7 @@ def main():
                    "width": W, "height": H, "spp": spp, "triangles": info["triangle_count"],
                    "bvh_depth": info["max_bvh_depth"], "parallelism": f"spp-split x{world}, RCCL reduce"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args),
                      "kernel": "render_kernel", "kernel_ms": round(avg_kernel_s * 1e3, 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests",

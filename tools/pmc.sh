@@ -5,7 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS=${PMC_BENCH_ARGS:-"--spp 32 --steps 1 --warmup 0 --no-cpu-baseline"}
+ARGS=${PMC_BENCH_ARGS:-"--steps 1 --warmup 0 --no-cpu-baseline"}
+echo "$ARGS" > gpurun_out/pmc/args.txt
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1
 echo "list rc=$?"
 run_pass() {

@@ -179,6 +179,14 @@ struct vr_scene {
     unsigned long long* d_counters = nullptr;
     std::mutex counter_mutex;
     std::atomic<uint64_t> pass_counter{0};
+    // per-sample staging buffer + work-queue counter, reused across calls; `staging_free` is
+    // recorded after the last kernel that reads them, and every new call's stream waits on it
+    std::mutex staging_mutex;
+    void* staging = nullptr;
+    size_t staging_bytes = 0;
+    unsigned long long* d_queue = nullptr;
+    hipEvent_t staging_free = nullptr;
+    int cu_count = 0;
     uint64_t partial_seed = 0x5EED0001ull;
 };
 
@@ -209,6 +217,9 @@ int upload(vr_scene* s) {
     }
     VR_HIP(hipMalloc(&s->d_block, total));
     s->device_bytes = total;
+    VR_HIP(hipDeviceGetAttribute(&s->cu_count, hipDeviceAttributeMultiprocessorCount, s->device));
+    VR_HIP(hipMalloc(&s->d_queue, 256));
+    VR_HIP(hipEventCreateWithFlags(&s->staging_free, hipEventDisableTiming));
     char* base = (char*)s->d_block;
     const void* src[6] = {s->nodes.data(), s->tris.data(), s->normals.data(), s->materials.data(), s->prims.data(),
                           s->bvhs.data()};
@@ -257,9 +268,14 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.state = state;
     a.records = nullptr;
     a.counters = nullptr;
+    a.wg_times = nullptr;
     a.error_flag = s->d_error;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 32u;
+    const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
+    a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 16u;
+    a.queue = s->d_queue;
+    a.staging = nullptr;
     return a;
 }
 
@@ -528,9 +544,15 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
 
 void vr_scene_destroy(vr_scene* s) {
     if (!s) return;
-    if (s->d_block) {
+    if (s->d_block || s->staging) {
         (void)hipSetDevice(s->device);
-        (void)hipFree(s->d_block);
+        if (s->staging_free) {
+            (void)hipEventSynchronize(s->staging_free);
+            (void)hipEventDestroy(s->staging_free);
+        }
+        if (s->staging) (void)hipFree(s->staging);
+        if (s->d_queue) (void)hipFree(s->d_queue);
+        if (s->d_block) (void)hipFree(s->d_block);
     }
     delete s;
 }
@@ -552,6 +574,48 @@ int vr_scene_bvh_leaf_order(const vr_scene* s, uint32_t mesh, uint64_t* out) {
     return VR_OK;
 }
 
+namespace {
+// Enqueue the render of params `p` into `state` on stream `st` in passes that fit the staging
+// buffer (24 B per pixel-sample).  Caller holds s->staging_mutex.
+int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStream_t st, bool counting,
+                   bool recording, void* records, unsigned long long* counters, unsigned long long* wg_times) {
+    const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
+    const uint64_t npix = tw * th;
+    if (npix == 0 || p->spp == 0) return VR_OK;
+    size_t free_b = 0, total_b = 0;
+    VR_HIP(hipMemGetInfo(&free_b, &total_b));
+    const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + s->staging_bytes) / 2);
+    uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (24 * npix)));
+    const size_t need = (size_t)(24 * npix * pass);
+    // previous users of the staging buffer must be done before it is reused or resized
+    VR_HIP(hipStreamWaitEvent(st, s->staging_free, 0));
+    if (need > s->staging_bytes) {
+        VR_HIP(hipEventSynchronize(s->staging_free));
+        if (s->staging) VR_HIP(hipFree(s->staging));
+        s->staging = nullptr;
+        s->staging_bytes = 0;
+        VR_HIP(hipMalloc(&s->staging, need));
+        s->staging_bytes = need;
+    }
+    for (uint64_t done = 0; done < p->spp; done += pass) {
+        vr_render_params q = *p;
+        q.spp = (uint32_t)std::min<uint64_t>(pass, p->spp - done);
+        q.first_sample = p->first_sample + done;
+        q.accumulate = (done > 0 || p->accumulate) ? 1u : 0u;
+        vr::RenderArgs a = make_args(s, &q, state);
+        a.staging = (double*)s->staging;
+        a.records = records;
+        a.counters = counters;
+        a.wg_times = done == 0 ? wg_times : nullptr;
+        VR_HIP(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), st));
+        int lr = vr::launch_render(a, stack_depth(s), counting, recording, s->dark0, std::max(1, s->cu_count) * 3, st);
+        if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    }
+    VR_HIP(hipEventRecord(s->staging_free, st));
+    return VR_OK;
+}
+}  // namespace
+
 int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats) {
     int rc = check_render_params(s, p);
@@ -564,10 +628,18 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     const bool counting = (launch_flags & VR_LAUNCH_COUNTERS) != 0;
     const bool timed = (launch_flags & VR_LAUNCH_TIMED) != 0 || counting;
     std::unique_lock<std::mutex> lock(ms->counter_mutex, std::defer_lock);
+    // diagnostic (tools): with counters, VR_WG_TIMES_PATH receives per-workgroup start/end stamps
+    const char* wg_path = counting ? getenv("VR_WG_TIMES_PATH") : nullptr;
+    CallScratch wg;
+    const uint64_t blocks = (uint64_t)std::max(1, s->cu_count) * 3;  // persistent grid limit
     if (counting) {
         lock.lock();
         VR_HIP(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long) * vr::kCntCount, st));
         a.counters = s->d_counters;
+        if (wg_path) {
+            VR_HIP(hipMalloc(&wg.ptr, blocks * 2 * sizeof(unsigned long long)));
+            a.wg_times = (unsigned long long*)wg.ptr;
+        }
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timed) {
@@ -575,8 +647,11 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         VR_HIP(hipEventCreate(&e1));
         VR_HIP(hipEventRecord(e0, st));
     }
-    int lr = vr::launch_render(a, stack_depth(s), counting, false, s->dark0, st);
-    if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    {
+        std::lock_guard<std::mutex> g(ms->staging_mutex);
+        int er = enqueue_passes(ms, p, state, st, counting, false, nullptr, a.counters, a.wg_times);
+        if (er) return er;
+    }
     if (timed) {
         VR_HIP(hipEventRecord(e1, st));
         VR_HIP(hipEventSynchronize(e1));
@@ -592,6 +667,14 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         if (counting) {
             unsigned long long c[vr::kCntCount];
             VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+            if (wg_path && wg.ptr) {
+                std::vector<unsigned long long> t(blocks * 2);
+                VR_HIP(hipMemcpy(t.data(), wg.ptr, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+                if (FILE* f = std::fopen(wg_path, "wb")) {
+                    std::fwrite(t.data(), sizeof(unsigned long long), t.size(), f);
+                    std::fclose(f);
+                }
+            }
             if (stats) {
                 stats->box_tests = c[vr::kCntBoxTests];
                 stats->node_visits = c[vr::kCntNodeVisits];
@@ -683,10 +766,12 @@ int vr_render_samples(const vr_scene* s, const vr_render_params* p, vr_sample_re
     VR_HIP(hipMalloc(&rec.ptr, rec_bytes));
     vr_render_params q = *p;
     q.accumulate = 0;
-    vr::RenderArgs a = make_args(s, &q, (double*)cs.ptr);
-    a.records = rec.ptr;
-    int lr = vr::launch_render(a, stack_depth(s), false, true, s->dark0, cs.stream);
-    if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+    {
+        vr_scene* ms = const_cast<vr_scene*>(s);
+        std::lock_guard<std::mutex> g(ms->staging_mutex);
+        int er = enqueue_passes(ms, &q, (double*)cs.ptr, cs.stream, false, true, rec.ptr, nullptr, nullptr);
+        if (er) return er;
+    }
     VR_HIP(hipMemcpyAsync(out, rec.ptr, rec_bytes, hipMemcpyDeviceToHost, cs.stream));
     VR_HIP(hipStreamSynchronize(cs.stream));
     return read_and_clear_error(s, cs.stream);

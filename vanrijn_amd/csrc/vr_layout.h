@@ -99,14 +99,17 @@ struct RenderArgs {
     DeviceScene scene;
     uint64_t start_column, start_row, tile_width, tile_height;
     uint64_t width, height;
-    uint64_t seed, first_sample;
-    uint32_t spp;
+    uint64_t seed, first_sample;  // absolute index of this pass's sample 0
+    uint32_t spp;                 // samples in this pass
     uint32_t accumulate;
-    uint32_t shade_threshold;  // v2: lanes finished with traversal before the wave shades
-    uint32_t pad;
-    double* state;             // [tile pixels][8]
+    uint32_t shade_threshold;     // lanes finished with traversal before the wave shades
+    uint32_t chunk;               // samples per work item (one pixel x `chunk` consecutive samples)
+    unsigned long long* queue;    // work-item counter (zeroed before the launch)
+    double* staging;              // [pass sample][tile pixel][3] XYZ of every sample
+    double* state;                // [tile pixels][8]
     void* records;             // vr_sample_record* (record variant) or nullptr
-    unsigned long long* counters;  // [8] (counting variant) or nullptr
+    unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
+    unsigned long long* wg_times;  // counting variant: [blocks][2] s_memrealtime at start / end, or nullptr
     int32_t* error_flag;
 };
 
@@ -134,7 +137,7 @@ enum Counter : int {
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
 int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0,
-                  void* stream);
+                  int grid_limit, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

@@ -39,38 +39,39 @@ namespace dev {
 __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}; }  // mod.rs:41-46
 
 // ----------------------------------------------------------------------------------------------
-// Render kernel: one pixel per lane, traversal and shading interleaved by phases.
+// Render kernel: persistent waves, lane-level work queue, traversal and shading interleaved.
 //
-// A first version traced one ray per lane per path-loop iteration, so a wave's traversal loop ran
-// as long as its longest ray (measured lane utilisation 25 %).  Here each lane's traversal state
-// (node, LDS stack, closest hit so far) stays alive across iterations: the wave steps BVH nodes
-// for all traversing lanes until at least `shade_threshold` lanes have finished, then those lanes
-// shade (BSDF, next bounce ray -- or the sample's end and the next sample's camera ray) and
-// rejoin the traversal while unfinished lanes resume where they stopped.  Kahan sums live in LDS
-// and the stack holds node indices only (a popped subtree is culled by its children's box tests).
+// Work items are (pixel, `chunk` consecutive samples), numbered chunk-major over 8x8 pixel
+// blocks.  Every lane pulls its own items (one wave-aggregated atomic per refill), so expensive
+// pixels (bunny, floor) never serialise behind a workgroup boundary: with whole 16x16 blocks x
+// 256 spp per workgroup, average workgroup concurrency was 43 % of the chip's (the most
+// expensive block alone ran 147 ms of a 293 ms launch).  Each sample's XYZ goes to a staging
+// buffer; accumulate_kernel then folds them per pixel in sample order with the reference's
+// Kahan update, so results are bit-identical to sequential update_pixel calls.
+//
+// Inside a wave, each lane's traversal state (node, LDS stack, closest hit) stays alive across
+// iterations: the wave steps BVH nodes for all traversing lanes until at least
+// `shade_threshold` lanes have finished, then those lanes shade (BSDF, next bounce ray -- or the
+// sample's end and the next camera ray) and rejoin.  (One-ray-per-iteration lock-step measured
+// 25 % traversal lane utilisation.)  The stack holds node indices only.
 // ----------------------------------------------------------------------------------------------
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
 
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MINW = 3>
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ uint32_t st_node[STACK * 256];
-    __shared__ double kahan[8 * 256];  // [sum x, sum y, sum z, bias x, bias y, bias z, weight, weight_bias][tid]
     const int tid = threadIdx.x;
+    const unsigned lane = __lane_id();
     const DeviceScene& S = A.scene;
-    uint32_t px, py;
-    {
-        const int wave = tid >> 6, lane = tid & 63;
-        const uint32_t bw = (uint32_t)((A.tile_width + 15) / 16);
-        px = (blockIdx.x % bw) * 16 + (wave & 1) * 8 + (lane & 7);
-        py = (blockIdx.x / bw) * 16 + (wave >> 1) * 8 + (lane >> 3);
-    }
-    const bool live = px < A.tile_width && py < A.tile_height;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t samples_done = 0;
-    for (int k = 0; k < 8; ++k)
-        kahan[k * 256 + tid] = (live && A.accumulate) ? A.state[((uint64_t)py * A.tile_width + px) * 8 + k] : 0.0;
-
-    int state = (live && A.spp > 0) ? kNeedRay : kDone;
+    if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
+    const uint64_t per_chunk = (uint64_t)bw * bh * 64;
+    const uint64_t items = per_chunk * ((A.spp + A.chunk - 1) / A.chunk);
+    const uint64_t npix = A.tile_width * A.tile_height;
+    uint32_t px = 0, py = 0, s_end = 0;
+    int state = kNeedRay;  // with s_idx == s_end: needs a work item
     uint32_t s_idx = 0;
     Rng rng;
     rng.base = 0;
@@ -149,27 +150,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         node = -1;
         state = start_bvhs() ? kTraversing : kTraversed;
     };
-    auto finish = [&](double wl, double I) {  // update_pixel(row, col, photon x 360, 1.0)
+    auto finish = [&](double wl, double I) {  // photon.scale_intensity(360) -> ColourXyz::from_photon
         const double Is = I * 360.0;
         const V3 c = xyz_for_wavelength(wl);
         const double cc[3] = {c.x * Is, c.y * Is, c.z * Is};
-        double* K = kahan + tid;
-        const double wsum = K[6 * 256], wbias = K[7 * 256];
-        const double wy = 1.0 - wbias;
-        const double wt = wsum + wy;
-        K[7 * 256] = (wt - wsum) - wy;
-        K[6 * 256] = wt;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const double sum = K[k * 256], bias = K[(3 + k) * 256];
-            const double y = cc[k] * 1.0 - bias;
-            const double t = sum + y;
-            K[(3 + k) * 256] = (t - sum) - y;
-            K[k * 256] = t;
-        }
+        double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 3;
+        out[0] = cc[0];
+        out[1] = cc[1];
+        out[2] = cc[2];
         if (RECORD) {
             vr_sample_record* rec =
-                (vr_sample_record*)A.records + (((uint64_t)py * A.tile_width + px) * A.spp + s_idx);
+                (vr_sample_record*)A.records + (((uint64_t)py * A.tile_width + px) * A.spp + s_idx);  // single pass
             rec->wavelength = wl;
             rec->intensity = I;
             rec->xyz[0] = cc[0];
@@ -304,26 +295,49 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 }
             }
         }
-        if (state == kNeedRay) {
-            if (s_idx == A.spp) {
-                state = kDone;
-            } else {
-                const uint64_t row = A.start_row + py, col = A.start_column + px;
-                rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
-                rng.k = 0;
-                // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
-                const double fw_d = (double)A.width, fh_d = (double)A.height;
-                const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
-                const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
-                const double ux = rng.standard();
-                const double uy = rng.standard();
-                const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
-                const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
-                depth = -1;
-                bounces = 0;
-                flags = 0;
-                begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
+        // refill: lanes whose item is exhausted take the next items (one atomic per wave)
+        while (true) {
+            const bool need = state == kNeedRay && s_idx >= s_end;
+            const uint64_t m = __ballot(need);
+            if (m == 0) break;
+            const unsigned leader = (unsigned)__builtin_ctzll(m);
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
+            base = __shfl(base, (int)leader);
+            if (need) {
+                const uint64_t g = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+                if (g >= items) {
+                    state = kDone;
+                } else {
+                    const uint32_t chunk_i = (uint32_t)(g / per_chunk);
+                    const uint64_t r = g - (uint64_t)chunk_i * per_chunk;
+                    const uint32_t blk = (uint32_t)(r >> 6), l = (uint32_t)(r & 63);
+                    const uint32_t x = (blk % bw) * 8 + (l & 7), y = (blk / bw) * 8 + (l >> 3);
+                    if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
+                        px = x;
+                        py = y;
+                        s_idx = chunk_i * A.chunk;
+                        s_end = min(A.spp, s_idx + A.chunk);
+                    }
+                }
             }
+        }
+        if (state == kNeedRay) {
+            const uint64_t row = A.start_row + py, col = A.start_column + px;
+            rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
+            rng.k = 0;
+            // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
+            const double fw_d = (double)A.width, fh_d = (double)A.height;
+            const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
+            const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
+            const double ux = rng.standard();
+            const double uy = rng.standard();
+            const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
+            const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
+            depth = -1;
+            bounces = 0;
+            flags = 0;
+            begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
         }
         if (__ballot(state != kDone) == 0) break;
         // ---------------------------------------------------------------- phase B: traverse
@@ -365,8 +379,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                  __popcll(__ballot(state == kTraversed)) < (int)A.shade_threshold);
     }
 
-    if (live)
-        for (int k = 0; k < 8; ++k) A.state[((uint64_t)py * A.tile_width + px) * 8 + k] = kahan[k * 256 + tid];
     if (COUNT) {
         atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
         atomicAdd(&A.counters[kCntNodeVisits], (unsigned long long)cnt.node_visits);
@@ -377,7 +389,48 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
         atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
         atomicAdd(&A.counters[kCntExactBoxes], (unsigned long long)cnt.exact_boxes);
+        if (A.wg_times) {
+            __syncthreads();
+            if (tid == 0) A.wg_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
+}
+
+// accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
+// order: the same Kahan sequence the reference applies call by call.
+__global__ __launch_bounds__(256) void accumulate_kernel(double* state, const double* staging, uint64_t npix,
+                                                         uint32_t spp, uint32_t accumulate) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    double sum[3] = {0.0, 0.0, 0.0}, bias[3] = {0.0, 0.0, 0.0}, w = 0.0, wb = 0.0;
+    if (accumulate) {
+        for (int k = 0; k < 3; ++k) {
+            sum[k] = state[p * 8 + k];
+            bias[k] = state[p * 8 + 3 + k];
+        }
+        w = state[p * 8 + 6];
+        wb = state[p * 8 + 7];
+    }
+    for (uint32_t s = 0; s < spp; ++s) {
+        const double* c = staging + ((uint64_t)s * npix + p) * 3;
+        const double wy = 1.0 - wb;
+        const double wt = w + wy;
+        wb = (wt - w) - wy;
+        w = wt;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double y = c[k] * 1.0 - bias[k];
+            const double t = sum[k] + y;
+            bias[k] = (t - sum[k]) - y;
+            sum[k] = t;
+        }
+    }
+    for (int k = 0; k < 3; ++k) {
+        state[p * 8 + k] = sum[k];
+        state[p * 8 + 3 + k] = bias[k];
+    }
+    state[p * 8 + 6] = w;
+    state[p * 8 + 7] = wb;
 }
 
 template <int STACK>
@@ -418,41 +471,49 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
 // Host-side launch wrappers
 // ----------------------------------------------------------------------------------------------
 template <int STACK>
-static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, hipStream_t s) {
-    const uint64_t blocks = ((a.tile_width + 15) / 16) * ((a.tile_height + 15) / 16);
-    dim3 grid((unsigned)blocks), block(256);
-    // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3:
-    // measured fastest, 168 VGPRs with a few cold spills; 2 and 4 are 15-20 % and 8 % slower)
+static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int grid_limit,
+                                  hipStream_t s) {
+    // persistent waves: enough workgroups to fill the chip, each wave loops over work items
+    const uint64_t items = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64 *
+                           ((a.spp + a.chunk - 1) / a.chunk);
+    const uint64_t want = (items + 255) / 256;
+    dim3 grid((unsigned)(want < (uint64_t)grid_limit ? want : (uint64_t)grid_limit)), block(256);
+    // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
     if (variant >= 1 && variant <= 4 && variant != 3 && !recording && !counting && dark0) {
         if (variant == 1) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 1>), grid, block, 0, s, a);
         if (variant == 2) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 2>), grid, block, 0, s, a);
-        if (variant == 3) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3>), grid, block, 0, s, a);
         if (variant == 4) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 4>), grid, block, 0, s, a);
-        return hipGetLastError();
-    }
-#define VR_LAUNCH(C, R, D) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D>), grid, block, 0, s, a)
-    if (dark0) {
-        if (recording) VR_LAUNCH(false, true, true);
-        else if (counting) VR_LAUNCH(true, false, true);
-        else VR_LAUNCH(false, false, true);
     } else {
-        if (recording) VR_LAUNCH(false, true, false);
-        else if (counting) VR_LAUNCH(true, false, false);
-        else VR_LAUNCH(false, false, false);
-    }
+#define VR_LAUNCH(C, R, D) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D>), grid, block, 0, s, a)
+        if (dark0) {
+            if (recording) VR_LAUNCH(false, true, true);
+            else if (counting) VR_LAUNCH(true, false, true);
+            else VR_LAUNCH(false, false, true);
+        } else {
+            if (recording) VR_LAUNCH(false, true, false);
+            else if (counting) VR_LAUNCH(true, false, false);
+            else VR_LAUNCH(false, false, false);
+        }
 #undef VR_LAUNCH
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t npix = a.tile_width * a.tile_height;
+    hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
+                       (const double*)a.staging, npix, a.spp, a.accumulate);
     return hipGetLastError();
 }
 
-int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, void* stream) {
+int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int grid_limit,
+                  void* stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (a.tile_width == 0 || a.tile_height == 0) return 0;
+    if (a.tile_width == 0 || a.tile_height == 0 || a.spp == 0) return 0;
     hipError_t e;
-    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, s);
-    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, s);
-    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, s);
+    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, grid_limit, s);
+    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, grid_limit, s);
+    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, grid_limit, s);
     else return -1000;
     return (int)e;
 }
