@@ -171,6 +171,7 @@ struct vr_scene {
     int max_depth = 0;
     uint32_t object_count = 0;
     bool dark0 = true;  // every material's colour(0 nm) == 0: the recursion-limit photon needs no lambda-0 chain
+    int mats = 0;       // bit 0: a Lambertian material exists, bit 1: a reflective one
     // device copies
     void* d_block = nullptr;
     size_t device_bytes = 0;
@@ -271,7 +272,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.wg_times = nullptr;
     a.error_flag = s->d_error;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
-    a.shade_threshold = th ? (uint32_t)atoi(th) : 32u;
+    a.shade_threshold = th ? (uint32_t)atoi(th) : 56u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
     a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 16u;
     a.queue = s->d_queue;
@@ -396,6 +397,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         std::memcpy(dm.samples, m.colour.samples, sizeof(double) * m.colour.sample_count);
         s->materials.push_back(dm);
         if (vr_spectrum_intensity_at_wavelength(&m.colour, 0.0) != 0.0) s->dark0 = false;
+        s->mats |= m.kind == VR_MATERIAL_REFLECTIVE ? 2 : 1;
     }
     // objects: primitive lists keep their order; BVHs are built per mesh
     std::vector<int> mesh_object(desc->mesh_count, -1);
@@ -576,7 +578,7 @@ int vr_scene_bvh_leaf_order(const vr_scene* s, uint32_t mesh, uint64_t* out) {
 
 namespace {
 // Enqueue the render of params `p` into `state` on stream `st` in passes that fit the staging
-// buffer (24 B per pixel-sample).  Caller holds s->staging_mutex.
+// buffer (16 B per pixel-sample: the final photon).  Caller holds s->staging_mutex.
 int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStream_t st, bool counting,
                    bool recording, void* records, unsigned long long* counters, unsigned long long* wg_times) {
     const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
@@ -585,8 +587,8 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
     size_t free_b = 0, total_b = 0;
     VR_HIP(hipMemGetInfo(&free_b, &total_b));
     const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + s->staging_bytes) / 2);
-    uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (24 * npix)));
-    const size_t need = (size_t)(24 * npix * pass);
+    uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (16 * npix)));
+    const size_t need = (size_t)(16 * npix * pass);
     // previous users of the staging buffer must be done before it is reused or resized
     VR_HIP(hipStreamWaitEvent(st, s->staging_free, 0));
     if (need > s->staging_bytes) {
@@ -608,7 +610,8 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;
         VR_HIP(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), st));
-        int lr = vr::launch_render(a, stack_depth(s), counting, recording, s->dark0, std::max(1, s->cu_count) * 3, st);
+        int lr = vr::launch_render(a, stack_depth(s), counting, recording, s->dark0, s->mats ? s->mats : 3,
+                                    std::max(1, s->cu_count) * 3, st);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
     }
     VR_HIP(hipEventRecord(s->staging_free, st));

@@ -105,7 +105,7 @@ struct RenderArgs {
     uint32_t shade_threshold;     // lanes finished with traversal before the wave shades
     uint32_t chunk;               // samples per work item (one pixel x `chunk` consecutive samples)
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
-    double* staging;              // [pass sample][tile pixel][3] XYZ of every sample
+    double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
     double* state;                // [tile pixels][8]
     void* records;             // vr_sample_record* (record variant) or nullptr
     unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
@@ -136,7 +136,7 @@ enum Counter : int {
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
-int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0,
+int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
                   int grid_limit, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);

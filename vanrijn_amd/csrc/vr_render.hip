@@ -57,7 +57,9 @@ __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}
 // ----------------------------------------------------------------------------------------------
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
 
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MINW = 3>
+// MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
+// compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3>
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ uint32_t st_node[STACK * 256];
     const int tid = threadIdx.x;
@@ -150,22 +152,22 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         node = -1;
         state = start_bvhs() ? kTraversing : kTraversed;
     };
-    auto finish = [&](double wl, double I) {  // photon.scale_intensity(360) -> ColourXyz::from_photon
-        const double Is = I * 360.0;
-        const V3 c = xyz_for_wavelength(wl);
-        const double cc[3] = {c.x * Is, c.y * Is, c.z * Is};
-        double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 3;
-        out[0] = cc[0];
-        out[1] = cc[1];
-        out[2] = cc[2];
+    // the sample's final photon goes to the staging buffer; accumulate_kernel turns it into XYZ
+    // (ColourXyz::from_photon of photon.scale_intensity(360)) and the Kahan sums
+    auto finish = [&](double wl, double I) {
+        double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
+        out[0] = wl;
+        out[1] = I;
         if (RECORD) {
+            const double Is = I * 360.0;
+            const V3 c = xyz_for_wavelength(wl);
             vr_sample_record* rec =
                 (vr_sample_record*)A.records + (((uint64_t)py * A.tile_width + px) * A.spp + s_idx);  // single pass
             rec->wavelength = wl;
             rec->intensity = I;
-            rec->xyz[0] = cc[0];
-            rec->xyz[1] = cc[1];
-            rec->xyz[2] = cc[2];
+            rec->xyz[0] = c.x * Is;
+            rec->xyz[1] = c.y * Is;
+            rec->xyz[2] = c.z * Is;
             rec->bounces = bounces;
             rec->flags = flags;
         }
@@ -194,7 +196,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         const Material* mat = &S.materials[h.material];
         V3 w_o;
         double pdf;
-        if (mat->kind == 1) {  // reflective_material.rs:42-47
+        const bool reflective = MATS == 2 || (MATS == 3 && mat->kind == 1);
+        if (reflective) {  // reflective_material.rs:42-47
             w_o = mk(-w_i.x, -w_i.y, w_i.z);
             pdf = 1.0;
         } else {  // lambertian_material.rs:36-59: rejection sampling on Open01 pairs
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         const double c_l = material_colour(mat, lambda);
         const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
         double a, a0, bterm;
-        if (mat->kind == 1) {  // reflective_material.rs:17-39
+        if (reflective) {  // reflective_material.rs:17-39
             if (w_i.z <= 0.0 || w_o.z <= 0.0) {
                 a = 0.0; a0 = 0.0; bterm = 0.0;
             } else {
@@ -412,7 +415,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
         wb = state[p * 8 + 7];
     }
     for (uint32_t s = 0; s < spp; ++s) {
-        const double* c = staging + ((uint64_t)s * npix + p) * 3;
+        const double* ph = staging + ((uint64_t)s * npix + p) * 2;  // final photon {wavelength, intensity}
+        const double Is = ph[1] * 360.0;                            // photon.rs:26-28, camera.rs:121-126
+        const V3 cx = xyz_for_wavelength(ph[0]);                    // colour_xyz.rs:31-35
+        const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
         const double wy = 1.0 - wb;
         const double wt = w + wy;
         wb = (wt - w) - wy;
@@ -471,8 +477,8 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
 // Host-side launch wrappers
 // ----------------------------------------------------------------------------------------------
 template <int STACK>
-static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int grid_limit,
-                                  hipStream_t s) {
+static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int mats,
+                                  int grid_limit, hipStream_t s) {
     // persistent waves: enough workgroups to fill the chip, each wave loops over work items
     const uint64_t items = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64 *
                            ((a.spp + a.chunk - 1) / a.chunk);
@@ -481,23 +487,26 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
-    if (variant >= 1 && variant <= 4 && variant != 3 && !recording && !counting && dark0) {
-        if (variant == 1) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 1>), grid, block, 0, s, a);
-        if (variant == 2) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 2>), grid, block, 0, s, a);
-        if (variant == 4) hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 4>), grid, block, 0, s, a);
+    if (!dark0) mats = 3;  // the general kernel
+#define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)
+#define VR_MODES(D, M)                                     \
+    if (recording) VR_LAUNCH(false, true, D, M, 3);        \
+    else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
+    else if (variant == 1) VR_LAUNCH(false, false, D, M, 1); \
+    else if (variant == 2) VR_LAUNCH(false, false, D, M, 2); \
+    else if (variant == 4) VR_LAUNCH(false, false, D, M, 4); \
+    else VR_LAUNCH(false, false, D, M, 3)
+    if (!dark0) {
+        VR_MODES(false, 3);
+    } else if (mats == 1) {
+        VR_MODES(true, 1);
+    } else if (mats == 2) {
+        VR_MODES(true, 2);
     } else {
-#define VR_LAUNCH(C, R, D) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D>), grid, block, 0, s, a)
-        if (dark0) {
-            if (recording) VR_LAUNCH(false, true, true);
-            else if (counting) VR_LAUNCH(true, false, true);
-            else VR_LAUNCH(false, false, true);
-        } else {
-            if (recording) VR_LAUNCH(false, true, false);
-            else if (counting) VR_LAUNCH(true, false, false);
-            else VR_LAUNCH(false, false, false);
-        }
-#undef VR_LAUNCH
+        VR_MODES(true, 3);
     }
+#undef VR_MODES
+#undef VR_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t npix = a.tile_width * a.tile_height;
@@ -506,14 +515,14 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     return hipGetLastError();
 }
 
-int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int grid_limit,
-                  void* stream) {
+int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int mats,
+                  int grid_limit, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (a.tile_width == 0 || a.tile_height == 0 || a.spp == 0) return 0;
     hipError_t e;
-    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, grid_limit, s);
-    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, grid_limit, s);
-    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, grid_limit, s);
+    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, mats, grid_limit, s);
+    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, mats, grid_limit, s);
+    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, mats, grid_limit, s);
     else return -1000;
     return (int)e;
 }
