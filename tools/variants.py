@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--thresholds", default="32")
     ap.add_argument("--scene", default="main")
+    ap.add_argument("--env", default="", help="NAME=v1,v2,... extra sweep over an environment variable")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     scene = scenes.main_scene() if a.scene == "main" else scenes.bench_scene()
@@ -32,21 +33,25 @@ def main():
     state = torch.zeros(W * H * 8, dtype=torch.float64, device="cuda")
     ref = None
     results = {}
-    combos = [(v, t) for v in a.variants.split(",") for t in a.thresholds.split(",")]
+    ename, evals = (a.env.split("=", 1)[0], a.env.split("=", 1)[1].split(",")) if a.env else ("", [""])
+    combos = [(v, t, e) for v in a.variants.split(",") for t in a.thresholds.split(",") for e in evals]
     for rep in range(a.reps):
-        for v, t in combos:
+        for v, t, e in combos:
             os.environ["VR_KERNEL_VARIANT"] = v
             os.environ["VR_SHADE_THRESHOLD"] = t
+            if ename:
+                os.environ[ename] = e
             st = render_tile_device(ds, Tile(0, W, 0, H), H, W, a.spp, 1, 0, state.data_ptr(),
                                     torch.cuda.current_stream().cuda_stream, timed=True)
             out = state.cpu()
             if ref is None:
                 ref = out
             same = bool(torch.equal(out, ref))
-            results.setdefault((v, t), []).append((st["kernel_ms"], same))
-    for (v, t), r in results.items():
+            results.setdefault((v, t, e), []).append((st["kernel_ms"], same))
+    for (v, t, e), r in results.items():
         ms = [x[0] for x in r]
-        print(json.dumps({"variant": v, "threshold": t, "median_ms": statistics.median(ms), "min_ms": min(ms),
+        print(json.dumps({"variant": v, "threshold": t, ename or "env": e, "scene": a.scene,
+                          "median_ms": statistics.median(ms), "min_ms": min(ms),
                           "msamples_s": W * H * a.spp / statistics.median(ms) / 1e3,
                           "bitwise_equal_to_first": all(x[1] for x in r)}), flush=True)
 

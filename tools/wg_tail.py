@@ -14,9 +14,10 @@ from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
 
 def main():
     spp = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    which = sys.argv[2] if len(sys.argv) > 2 else "main"
     path = "/tmp/wg_times.bin"
     os.environ["VR_WG_TIMES_PATH"] = path
-    ds = scenes.main_scene().device_scene(0)
+    ds = (scenes.main_scene() if which == "main" else scenes.bench_scene()).device_scene(0)
     W = H = 1024
     state = torch.zeros(W * H * 8, dtype=torch.float64, device="cuda")
     st = render_tile_device(ds, Tile(0, W, 0, H), H, W, spp, 1, 0, state.data_ptr(),
@@ -31,7 +32,7 @@ def main():
     peak = active.max()
     # time after which fewer than half the peak workgroups are running
     half = grid[np.argmax((active < peak / 2) & (grid > grid[np.argmax(active)]))]
-    out = {"spp": spp, "kernel_ms": st["kernel_ms"], "makespan_ms": makespan / 1e6, "blocks": len(s),
+    out = {"scene": which, "spp": spp, "kernel_ms": st["kernel_ms"], "makespan_ms": makespan / 1e6, "blocks": len(s),
            "peak_concurrent": int(peak), "mean_concurrent": float(active.mean()),
            "utilisation": float(active.mean() / peak), "tail_start_ms": float(half / 1e6),
            "wg_ms_p50": float(np.median(dur) / 1e6), "wg_ms_p99": float(np.percentile(dur, 99) / 1e6),

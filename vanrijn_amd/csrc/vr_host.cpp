@@ -275,6 +275,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.shade_threshold = th ? (uint32_t)atoi(th) : 56u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
     a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 16u;
+    const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
+    a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     a.queue = s->d_queue;
     a.staging = nullptr;
     return a;

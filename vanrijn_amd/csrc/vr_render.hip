@@ -274,73 +274,79 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
 
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
-        if (COUNT && first_active_lane()) cnt.outer_slots += 64;
-        if (state == kTraversed) {
-            if (depth < 0) {
-                if (!best.kind) {
-                    finish(0.0, 0.0);  // camera ray missed: photon {0, 0} (camera.rs:110-113)
+        // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
+        // that only meet the plane or spheres), so those lanes do not idle through phase B
+        for (int rep = 0; rep < A.phase_a_reps; ++rep) {
+            if (COUNT && first_active_lane()) cnt.outer_slots += 64;
+            if (state == kTraversed) {
+                if (depth < 0) {
+                    if (!best.kind) {
+                        finish(0.0, 0.0);  // camera ray missed: photon {0, 0} (camera.rs:110-113)
+                    } else {
+                        flags |= 1;
+                        lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
+                        T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0; b0 = 0.0;
+                        depth = 0;
+                        shade();
+                    }
+                } else if (!best.kind) {
+                    finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
                 } else {
-                    flags |= 1;
-                    lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
-                    T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0; b0 = 0.0;
-                    depth = 0;
-                    shade();
-                }
-            } else if (!best.kind) {
-                finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
-            } else {
-                depth += 1;
-                if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
-                    flags |= 2;
-                    finish(0.0, DARK0 ? b0 : Acc0);
-                } else {
-                    shade();
-                }
-            }
-        }
-        // refill: lanes whose item is exhausted take the next items (one atomic per wave)
-        while (true) {
-            const bool need = state == kNeedRay && s_idx >= s_end;
-            const uint64_t m = __ballot(need);
-            if (m == 0) break;
-            const unsigned leader = (unsigned)__builtin_ctzll(m);
-            unsigned long long base = 0;
-            if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
-            base = __shfl(base, (int)leader);
-            if (need) {
-                const uint64_t g = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
-                if (g >= items) {
-                    state = kDone;
-                } else {
-                    const uint32_t chunk_i = (uint32_t)(g / per_chunk);
-                    const uint64_t r = g - (uint64_t)chunk_i * per_chunk;
-                    const uint32_t blk = (uint32_t)(r >> 6), l = (uint32_t)(r & 63);
-                    const uint32_t x = (blk % bw) * 8 + (l & 7), y = (blk / bw) * 8 + (l >> 3);
-                    if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
-                        px = x;
-                        py = y;
-                        s_idx = chunk_i * A.chunk;
-                        s_end = min(A.spp, s_idx + A.chunk);
+                    depth += 1;
+                    if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
+                        flags |= 2;
+                        finish(0.0, DARK0 ? b0 : Acc0);
+                    } else {
+                        shade();
                     }
                 }
             }
-        }
-        if (state == kNeedRay) {
-            const uint64_t row = A.start_row + py, col = A.start_column + px;
-            rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
-            rng.k = 0;
-            // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
-            const double fw_d = (double)A.width, fh_d = (double)A.height;
-            const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
-            const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
-            const double ux = rng.standard();
-            const double uy = rng.standard();
-            const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
-            const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
-            depth = -1;
-            bounces = 0;
-            flags = 0;
-            begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
+            // refill: lanes whose item is exhausted take the next items (one atomic per wave)
+            while (true) {
+                const bool need = state == kNeedRay && s_idx >= s_end;
+                const uint64_t m = __ballot(need);
+                if (m == 0) break;
+                const unsigned leader = (unsigned)__builtin_ctzll(m);
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
+                base = __shfl(base, (int)leader);
+                if (need) {
+                    const uint64_t g = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+                    if (g >= items) {
+                        state = kDone;
+                    } else {
+                        const uint32_t chunk_i = (uint32_t)(g / per_chunk);
+                        const uint64_t r = g - (uint64_t)chunk_i * per_chunk;
+                        const uint32_t blk = (uint32_t)(r >> 6), l = (uint32_t)(r & 63);
+                        const uint32_t x = (blk % bw) * 8 + (l & 7), y = (blk / bw) * 8 + (l >> 3);
+                        if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
+                            px = x;
+                            py = y;
+                            s_idx = chunk_i * A.chunk;
+                            s_end = min(A.spp, s_idx + A.chunk);
+                        }
+                    }
+                }
+            }
+            if (state == kNeedRay) {
+                const uint64_t row = A.start_row + py, col = A.start_column + px;
+                rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
+                rng.k = 0;
+                // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
+                const double fw_d = (double)A.width, fh_d = (double)A.height;
+                const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
+                const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
+                const double ux = rng.standard();
+                const double uy = rng.standard();
+                const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
+                const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
+                depth = -1;
+                bounces = 0;
+                flags = 0;
+                begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
+            }
+
+            if (__ballot(state == kTraversed) == 0) break;
         }
         if (__ballot(state != kDone) == 0) break;
         // ---------------------------------------------------------------- phase B: traverse
@@ -488,6 +494,7 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
     if (!dark0) mats = 3;  // the general kernel
+    if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);  // experiment hook
 #define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
