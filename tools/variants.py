@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--thresholds", default="32")
     ap.add_argument("--scene", default="main")
-    ap.add_argument("--env", default="", help="NAME=v1,v2,... extra sweep over an environment variable")
+    ap.add_argument("--env", action="append", default=[],
+                    help="NAME=v1,v2,... sweep over an environment variable (repeatable: cartesian product)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     scene = scenes.main_scene() if a.scene == "main" else scenes.bench_scene()
@@ -33,14 +34,16 @@ def main():
     state = torch.zeros(W * H * 8, dtype=torch.float64, device="cuda")
     ref = None
     results = {}
-    ename, evals = (a.env.split("=", 1)[0], a.env.split("=", 1)[1].split(",")) if a.env else ("", [""])
+    import itertools
+    names = [x.split("=", 1)[0] for x in a.env]
+    evals = list(itertools.product(*[x.split("=", 1)[1].split(",") for x in a.env]))
     combos = [(v, t, e) for v in a.variants.split(",") for t in a.thresholds.split(",") for e in evals]
     for rep in range(a.reps):
         for v, t, e in combos:
             os.environ["VR_KERNEL_VARIANT"] = v
             os.environ["VR_SHADE_THRESHOLD"] = t
-            if ename:
-                os.environ[ename] = e
+            for n, val in zip(names, e):
+                os.environ[n] = val
             st = render_tile_device(ds, Tile(0, W, 0, H), H, W, a.spp, 1, 0, state.data_ptr(),
                                     torch.cuda.current_stream().cuda_stream, timed=True)
             out = state.cpu()
@@ -50,7 +53,7 @@ def main():
             results.setdefault((v, t, e), []).append((st["kernel_ms"], same))
     for (v, t, e), r in results.items():
         ms = [x[0] for x in r]
-        print(json.dumps({"variant": v, "threshold": t, ename or "env": e, "scene": a.scene,
+        print(json.dumps({"variant": v, "threshold": t, **dict(zip(names, e)), "scene": a.scene,
                           "median_ms": statistics.median(ms), "min_ms": min(ms),
                           "msamples_s": W * H * a.spp / statistics.median(ms) / 1e3,
                           "bitwise_equal_to_first": all(x[1] for x in r)}), flush=True)

@@ -274,7 +274,12 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 56u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
-    a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 16u;
+    a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 1u;
+    const char* ts = getenv("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end
+    a.tail_samples = ts ? (uint32_t)std::max(0, atoi(ts)) : 0u;
+    const char* gr = getenv("VR_GRAB");  // tuning hook: items per queue atomic
+    a.grab = gr ? (uint32_t)std::max(0, atoi(gr)) : 512u;
+    a.pad3 = 0;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     a.queue = s->d_queue;

@@ -105,7 +105,9 @@ struct RenderArgs {
     uint32_t shade_threshold;     // lanes finished with traversal before the wave shades
     uint32_t chunk;               // samples per work item (one pixel x `chunk` consecutive samples)
     uint32_t phase_a_reps;        // max shade/generate rounds before traversal resumes
-    uint32_t pad2;
+    uint32_t tail_samples;        // the launch's last samples go out as single-sample items
+    uint32_t grab;                // items a wave takes from the queue per atomic (0: exactly its need)
+    uint32_t pad3;
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
     double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
     double* state;                // [tile pixels][8]

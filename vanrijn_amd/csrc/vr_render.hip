@@ -55,6 +55,27 @@ __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}
 // sample's end and the next camera ray) and rejoin.  (One-ray-per-iteration lock-step measured
 // 25 % traversal lane utilisation.)  The stack holds node indices only.
 // ----------------------------------------------------------------------------------------------
+// Items of one launch: the first spp - tail samples in chunks of `chunk`, then the last `tail`
+// samples one per item, so that a path that runs to the recursion limit near the end of the
+// launch holds one lane for one path, not for `chunk` of them.
+// keeps a wave-uniform 64-bit value in SGPRs
+__device__ inline uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__host__ __device__ inline uint32_t tail_of(const RenderArgs& a) {
+    return a.tail_samples < a.spp ? a.tail_samples : a.spp;
+}
+__host__ __device__ inline uint64_t chunk_rounds(const RenderArgs& a) {
+    const uint32_t bulk = a.spp - tail_of(a);
+    return (bulk + a.chunk - 1) / a.chunk;
+}
+__host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t per_chunk) {
+    return per_chunk * (chunk_rounds(a) + tail_of(a));
+}
+
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
 
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
@@ -70,11 +91,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
     const uint64_t per_chunk = (uint64_t)bw * bh * 64;
-    const uint64_t items = per_chunk * ((A.spp + A.chunk - 1) / A.chunk);
+    const uint64_t items = render_items(A, per_chunk);
+    const uint64_t rounds = chunk_rounds(A);
+    const uint32_t bulk = A.spp - tail_of(A);
     const uint64_t npix = A.tile_width * A.tile_height;
     uint32_t px = 0, py = 0, s_end = 0;
     int state = kNeedRay;  // with s_idx == s_end: needs a work item
     uint32_t s_idx = 0;
+    uint64_t w_next = 0, w_end = 0;  // this wave's slice of the queue (grab > 0)
     Rng rng;
     rng.base = 0;
     rng.k = 0;
@@ -307,11 +331,27 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 const uint64_t m = __ballot(need);
                 if (m == 0) break;
                 const unsigned leader = (unsigned)__builtin_ctzll(m);
+                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
-                base = __shfl(base, (int)leader);
-                if (need) {
-                    const uint64_t g = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+                bool take = need;
+                if (A.grab == 0) {
+                    if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)__popcll(m));
+                    base = __shfl(base, (int)leader);
+                } else {
+                    // wave-private slice of the queue: one atomic per `grab` items
+                    if (w_next >= w_end) {
+                        if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)A.grab);
+                        w_next = uniform64(__shfl(base, (int)leader));
+                        w_end = w_next + A.grab;
+                    }
+                    const uint64_t avail = w_end - w_next;
+                    base = w_next;
+                    take = need && rank < avail;
+                    const uint64_t want = (uint64_t)__popcll(m);
+                    w_next = uniform64(w_next + (want < avail ? want : avail));
+                }
+                if (take) {
+                    const uint64_t g = base + rank;
                     if (g >= items) {
                         state = kDone;
                     } else {
@@ -322,8 +362,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                         if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
                             px = x;
                             py = y;
-                            s_idx = chunk_i * A.chunk;
-                            s_end = min(A.spp, s_idx + A.chunk);
+                            if (chunk_i < rounds) {
+                                s_idx = chunk_i * A.chunk;
+                                s_end = min(bulk, s_idx + A.chunk);
+                            } else {
+                                s_idx = bulk + (uint32_t)(chunk_i - rounds);
+                                s_end = s_idx + 1;
+                            }
                         }
                     }
                 }
@@ -486,8 +531,7 @@ template <int STACK>
 static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int mats,
                                   int grid_limit, hipStream_t s) {
     // persistent waves: enough workgroups to fill the chip, each wave loops over work items
-    const uint64_t items = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64 *
-                           ((a.spp + a.chunk - 1) / a.chunk);
+    const uint64_t items = dev::render_items(a, ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64);
     const uint64_t want = (items + 255) / 256;
     dim3 grid((unsigned)(want < (uint64_t)grid_limit ? want : (uint64_t)grid_limit)), block(256);
     // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
