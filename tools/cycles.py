@@ -1,0 +1,29 @@
+"""Per-section wave clock cycles of the render kernel's counting variant (diagnostic).
+    python tools/cycles.py [spp] [scene]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vanrijn_amd import scenes  # noqa: E402
+from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
+
+SECTIONS = ["shade", "refill", "camera", "node_step", "leaf_tests", "stack_loop"]
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+which = sys.argv[2] if len(sys.argv) > 2 else "main"
+torch.cuda.set_device(0)
+ds = (scenes.main_scene() if which == "main" else scenes.bench_scene()).device_scene(0)
+state = torch.zeros(1024 * 1024 * 8, dtype=torch.float64, device="cuda")
+path = os.path.join("gpurun_out", "counters.bin")
+os.environ["VR_COUNTERS_PATH"] = path
+st = render_tile_device(ds, Tile(0, 1024, 0, 1024), 1024, 1024, spp, 1, 0, state.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream, counters=True)
+c = np.fromfile(path, dtype=np.uint64)
+cyc = c[9:15].astype(np.float64)
+out = {"scene": which, "spp": spp, "kernel_ms": st["kernel_ms"],
+       "cycles_share": {k: round(float(v / cyc.sum()), 4) for k, v in zip(SECTIONS, cyc)},
+       "cycles_total": float(cyc.sum()), "counters": {k: st[k] for k in st if k not in ("kernel_ms", "timed")}}
+print(json.dumps(out))

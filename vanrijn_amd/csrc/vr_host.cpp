@@ -282,6 +282,16 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.pad3 = 0;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
+    {
+        // same f64 operations as the reference's ImageSampler::new / film_to_world
+        const double fw = (double)a.width, fh = (double)a.height;
+        const double film_w = fw > fh ? fw / fh : 1.0;
+        const double film_h = fw > fh ? 1.0 : fw / fh;
+        a.film[0] = film_w * (1.0 / fw);
+        a.film[1] = film_w * 0.5;
+        a.film[2] = film_h * (1.0 / fh);
+        a.film[3] = film_h * 0.5;
+    }
     a.queue = s->d_queue;
     a.staging = nullptr;
     return a;
@@ -677,6 +687,12 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         if (counting) {
             unsigned long long c[vr::kCntCount];
             VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+            if (const char* cp = getenv("VR_COUNTERS_PATH")) {  // diagnostic: the raw counter array
+                if (FILE* f = std::fopen(cp, "wb")) {
+                    std::fwrite(c, sizeof c, 1, f);
+                    std::fclose(f);
+                }
+            }
             if (wg_path && wg.ptr) {
                 std::vector<unsigned long long> t(blocks * 2);
                 VR_HIP(hipMemcpy(t.data(), wg.ptr, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));

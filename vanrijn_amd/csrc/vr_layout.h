@@ -108,6 +108,9 @@ struct RenderArgs {
     uint32_t tail_samples;        // the launch's last samples go out as single-sample items
     uint32_t grab;                // items a wave takes from the queue per atomic (0: exactly its need)
     uint32_t pad3;
+    // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
+    // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
+    double film[4];
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
     double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
     double* state;                // [tile pixels][8]
@@ -136,6 +139,8 @@ enum Counter : int {
     kCntTraversalSlots = 6,  // 64 x wave-level traversal-loop iterations (lane-slot occupancy)
     kCntOuterSlots = 7,      // 64 x wave-level path-loop iterations
     kCntExactBoxes = 8,      // f32 box tests that fell back to the exact f64 test
+    kCntCycles = 9,          // 9..14: wave clock cycles per section (diagnostic, VR_COUNTERS_PATH):
+                             // shade, refill, camera, node step, leaf tests, stack/loop
     kCntCount = 16
 };
 

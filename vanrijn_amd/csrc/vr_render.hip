@@ -76,7 +76,9 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
     return per_chunk * (chunk_rounds(a) + tail_of(a));
 }
 
-enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3 };
+// kRayReady: the lane's next ray (ray_o, ray_d) is set and begin_ray runs once for all such
+// lanes at the end of phase A (one inlined copy for bounce and camera rays alike)
+enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
@@ -87,6 +89,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     const unsigned lane = __lane_id();
     const DeviceScene& S = A.scene;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t cyc[6] = {0, 0, 0, 0, 0, 0}, tprev = COUNT ? __builtin_amdgcn_s_memtime() : 0;
+#define VR_STAMP(i)                                           \
+    if (COUNT) {                                              \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        cyc[i] += t_ - tprev;                                 \
+        tprev = t_;                                           \
+    }
     uint32_t samples_done = 0;
     if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
@@ -108,6 +117,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
+    V3 ray_o = mk(0.0, 0.0, 0.0), ray_d = mk(0.0, 0.0, 1.0);  // next ray (state kRayReady)
 
     // BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
     auto culled = [&](double tlo, double thi) {
@@ -293,7 +303,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         wo_y = wo_world.y;
         const V3 d1 = normalize(wo_world);
         ++bounces;
-        begin_ray(add(h.loc, scl(d1, kBounceBias)), normalize(d1));
+        ray_o = add(h.loc, scl(d1, kBounceBias));
+        ray_d = normalize(d1);
+        state = kRayReady;
     };
 
     while (true) {
@@ -302,6 +314,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         // that only meet the plane or spheres), so those lanes do not idle through phase B
         for (int rep = 0; rep < A.phase_a_reps; ++rep) {
             if (COUNT && first_active_lane()) cnt.outer_slots += 64;
+            VR_STAMP(5);
             if (state == kTraversed) {
                 if (depth < 0) {
                     if (!best.kind) {
@@ -325,6 +338,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                     }
                 }
             }
+            VR_STAMP(0);
             // refill: lanes whose item is exhausted take the next items (one atomic per wave)
             while (true) {
                 const bool need = state == kNeedRay && s_idx >= s_end;
@@ -373,23 +387,26 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                     }
                 }
             }
+            VR_STAMP(1);
             if (state == kNeedRay) {
                 const uint64_t row = A.start_row + py, col = A.start_column + px;
                 rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
                 rng.k = 0;
                 // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
-                const double fw_d = (double)A.width, fh_d = (double)A.height;
-                const double film_w = fw_d > fh_d ? fw_d / fh_d : 1.0;
-                const double film_h = fw_d > fh_d ? 1.0 : fw_d / fh_d;
+                // film_w * (1 / w), film_w * 0.5, ... are per-launch constants (host: make_args)
                 const double ux = rng.standard();
                 const double uy = rng.standard();
-                const double x = ((double)col + ux) * (film_w * (1.0 / fw_d)) - film_w * 0.5;
-                const double y = ((double)(A.height - (row + 1)) + uy) * (film_h * (1.0 / fh_d)) - film_h * 0.5;
+                const double x = ((double)col + ux) * A.film[0] - A.film[1];
+                const double y = ((double)(A.height - (row + 1)) + uy) * A.film[2] - A.film[3];
                 depth = -1;
                 bounces = 0;
                 flags = 0;
-                begin_ray(mk(S.camera[0], S.camera[1], S.camera[2]), normalize(mk(x, y, 1.0)));
+                ray_o = mk(S.camera[0], S.camera[1], S.camera[2]);
+                ray_d = normalize(mk(x, y, 1.0));
+                state = kRayReady;
             }
+            if (state == kRayReady) begin_ray(ray_o, ray_d);
+            VR_STAMP(2);
 
             if (__ballot(state == kTraversed) == 0) break;
         }
@@ -397,6 +414,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         // ---------------------------------------------------------------- phase B: traverse
         do {
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
+            VR_STAMP(5);
             if (state == kTraversing) {
                 const Node32& nd = S.nodes32[node];
                 if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
@@ -410,8 +428,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 if (r1 == 2) { if (COUNT) cnt.exact_boxes++; h1 = slab(S.nodes[node].box[1], pre, lo1, hi1); }
                 h0 = h0 && !culled(lo0, hi0);
                 h1 = h1 && !culled(lo1, hi1);
+                VR_STAMP(3);
                 if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
                 if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
+                VR_STAMP(4);
                 if (h0 && h1) {
                     const bool swap = lo1 < lo0;  // near child first
                     st_node[sp * 256 + tid] = (uint32_t)(swap ? c0 : c1);
@@ -443,12 +463,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         atomicAdd(&A.counters[kCntTraversalSlots], (unsigned long long)cnt.trav_slots);
         atomicAdd(&A.counters[kCntOuterSlots], (unsigned long long)cnt.outer_slots);
         atomicAdd(&A.counters[kCntExactBoxes], (unsigned long long)cnt.exact_boxes);
+        VR_STAMP(5);
+        if (first_active_lane())
+            for (int i = 0; i < 6; ++i) atomicAdd(&A.counters[kCntCycles + i], (unsigned long long)cyc[i]);
         if (A.wg_times) {
             __syncthreads();
             if (tid == 0) A.wg_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
+
+#undef VR_STAMP
 
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
