@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vanrijn_amd import scenes  # noqa: E402
 from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
 
-SECTIONS = ["shade", "refill", "camera", "node_step", "leaf_tests", "stack_loop"]
+SECTIONS = ["shade", "refill", "camera_begin_ray", "node_step", "leaf_tests", "stack_loop"]
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 which = sys.argv[2] if len(sys.argv) > 2 else "main"
 torch.cuda.set_device(0)
@@ -25,5 +25,8 @@ c = np.fromfile(path, dtype=np.uint64)
 cyc = c[9:15].astype(np.float64)
 out = {"scene": which, "spp": spp, "kernel_ms": st["kernel_ms"],
        "cycles_share": {k: round(float(v / cyc.sum()), 4) for k, v in zip(SECTIONS, cyc)},
-       "cycles_total": float(cyc.sum()), "counters": {k: st[k] for k in st if k not in ("kernel_ms", "timed")}}
+       "cycles_total": float(cyc.sum()),
+       "wave_executions": {k: int(v) for k, v in zip(["leaf_test", "leaf_test_2nd", "exact_box", "shade", "camera",
+                                                        "begin_ray", "finish", "refill", "start_bvhs_trav"],
+                                                       c[15:24])}, "counters": {k: st[k] for k in st if k not in ("kernel_ms", "timed")}}
 print(json.dumps(out))

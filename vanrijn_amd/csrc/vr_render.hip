@@ -89,6 +89,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     const unsigned lane = __lane_id();
     const DeviceScene& S = A.scene;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t sec[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define VR_SEC(i) \
+    if (COUNT && first_active_lane()) sec[i]++;
     uint64_t cyc[6] = {0, 0, 0, 0, 0, 0}, tprev = COUNT ? __builtin_amdgcn_s_memtime() : 0;
 #define VR_STAMP(i)                                           \
     if (COUNT) {                                              \
@@ -189,6 +192,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     // the sample's final photon goes to the staging buffer; accumulate_kernel turns it into XYZ
     // (ColourXyz::from_photon of photon.scale_intensity(360)) and the Kahan sums
     auto finish = [&](double wl, double I) {
+        VR_SEC(6);
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
         out[0] = wl;
         out[1] = I;
@@ -212,6 +216,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     // one level of SimpleRandomIntegrator::integrate (simple_random_integrator.rs:20-53) at the
     // closest hit, forward form: returns true when a bounce ray was started
     auto shade = [&]() {
+        VR_SEC(3);
         HitInfo h;
         hit_info(S, best, pre, h);
         if (COUNT && best.kind == kTri) cnt.shaded++;
@@ -344,6 +349,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 const bool need = state == kNeedRay && s_idx >= s_end;
                 const uint64_t m = __ballot(need);
                 if (m == 0) break;
+                VR_SEC(7);
                 const unsigned leader = (unsigned)__builtin_ctzll(m);
                 const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
                 unsigned long long base = 0;
@@ -393,6 +399,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
                 rng.k = 0;
                 // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
+                VR_SEC(4);
                 // film_w * (1 / w), film_w * 0.5, ... are per-launch constants (host: make_args)
                 const double ux = rng.standard();
                 const double uy = rng.standard();
@@ -405,7 +412,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 ray_d = normalize(mk(x, y, 1.0));
                 state = kRayReady;
             }
-            if (state == kRayReady) begin_ray(ray_o, ray_d);
+            if (state == kRayReady) {
+                VR_SEC(5);
+                begin_ray(ray_o, ray_d);
+            }
             VR_STAMP(2);
 
             if (__ballot(state == kTraversed) == 0) break;
@@ -424,14 +434,23 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 const int r1 = slab32(nd.box[1], pre32, f1, g1);
                 double lo0 = f0, hi0 = g0, lo1 = f1, hi1 = g1;
                 bool h0 = r0 == 1, h1 = r1 == 1;
+                if (r0 == 2 || r1 == 2) { VR_SEC(2); }
                 if (r0 == 2) { if (COUNT) cnt.exact_boxes++; h0 = slab(S.nodes[node].box[0], pre, lo0, hi0); }
                 if (r1 == 2) { if (COUNT) cnt.exact_boxes++; h1 = slab(S.nodes[node].box[1], pre, lo1, hi1); }
                 h0 = h0 && !culled(lo0, hi0);
                 h1 = h1 && !culled(lo1, hi1);
-                VR_STAMP(3);
-                if (h0 && c0 < 0) { test_tri(~c0); h0 = false; }
-                if (h1 && c1 < 0) { test_tri(~c1); h1 = false; }
-                VR_STAMP(4);
+                // leaf children: one inlined triangle test, run once or twice
+                int ta = -1, tb = -1;
+                if (h0 && c0 < 0) { ta = ~c0; h0 = false; }
+                if (h1 && c1 < 0) { if (ta < 0) ta = ~c1; else tb = ~c1; h1 = false; }
+                bool second = false;
+                while (ta >= 0) {
+                    if (second) { VR_SEC(1); } else { VR_SEC(0); }
+                    second = true;
+                    test_tri(ta);
+                    ta = tb;
+                    tb = -1;
+                }
                 if (h0 && h1) {
                     const bool swap = lo1 < lo0;  // near child first
                     st_node[sp * 256 + tid] = (uint32_t)(swap ? c0 : c1);
@@ -445,6 +464,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                     --sp;
                     node = (int)st_node[sp * 256 + tid];
                 } else {
+                    VR_SEC(8);
                     ++bvh_i;
                     if (!start_bvhs()) state = kTraversed;
                 }
@@ -466,6 +486,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         VR_STAMP(5);
         if (first_active_lane())
             for (int i = 0; i < 6; ++i) atomicAdd(&A.counters[kCntCycles + i], (unsigned long long)cyc[i]);
+        for (int i = 0; i < 9; ++i)  // each lane counted the executions it led
+            if (sec[i]) atomicAdd(&A.counters[kCntSections + i], (unsigned long long)sec[i]);
         if (A.wg_times) {
             __syncthreads();
             if (tid == 0) A.wg_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -474,6 +496,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
 }
 
 #undef VR_STAMP
+#undef VR_SEC
 
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
