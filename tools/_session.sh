@@ -1,8 +1,6 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 300 python tools/cycles.py 64 main > gpurun_out/cycles.jsonl 2> gpurun_out/cycles.err
+timeout -k 10 700 python tools/variants.py --scene main --spp 256 --reps 2 --variants 0 --thresholds 48,56,60 > gpurun_out/ab.jsonl 2>> gpurun_out/variants.err
 rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python tools/cycles.py 32 bench >> gpurun_out/cycles.jsonl 2>> gpurun_out/cycles.err
-rc=$?; echo "rc=$rc"; cat gpurun_out/cycles.jsonl
-timeout -k 10 700 python tools/variants.py --scene main --spp 256 --reps 2 --variants 0 --thresholds 56 > gpurun_out/ab.jsonl 2>> gpurun_out/variants.err
+timeout -k 10 300 python tools/variants.py --scene bench --spp 32 --reps 3 --variants 0 --thresholds 56 >> gpurun_out/ab.jsonl 2>> gpurun_out/variants.err
 rc=$?; echo "rc=$rc"; cut -c 1-190 gpurun_out/ab.jsonl

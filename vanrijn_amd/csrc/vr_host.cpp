@@ -279,7 +279,11 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.tail_samples = ts ? (uint32_t)std::max(0, atoi(ts)) : 0u;
     const char* gr = getenv("VR_GRAB");  // tuning hook: items per queue atomic
     a.grab = gr ? (uint32_t)std::max(0, atoi(gr)) : 512u;
-    a.pad3 = 0;
+    const char* lt = getenv("VR_LEAF_THRESHOLD");  // tuning hooks
+    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 64u;
+    const char* ls = getenv("VR_LEAF_STALL");
+    a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 2u;
+    a.pad4 = 0;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {

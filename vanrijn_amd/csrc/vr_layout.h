@@ -107,7 +107,9 @@ struct RenderArgs {
     uint32_t phase_a_reps;        // max shade/generate rounds before traversal resumes
     uint32_t tail_samples;        // the launch's last samples go out as single-sample items
     uint32_t grab;                // items a wave takes from the queue per atomic (0: exactly its need)
-    uint32_t pad3;
+    uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
+    uint32_t leaf_stall;          // ... or this many lanes cannot step without one
+    uint32_t pad4;
     // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
     // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
     double film[4];

@@ -118,6 +118,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     Ray32 pre32;
     Best best;
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
+    // leaf triangles met during traversal wait here (p0 first) for a leaf round, in which every
+    // lane with one tests it: the f64 triangle test then runs for many lanes at once instead of
+    // for the few that reached a leaf in this step
+    int np = 0, p0 = -1, p1 = -1, p2 = -1, p3 = -1;
+    // f32 forms of the cull thresholds: cull_far >= bound + margin (rounded up), cull_behind <=
+    // -behind_margin (rounded down; -inf when behind-culling is off) -- never tighter than f64
+    float cull_far = INFINITY, cull_behind = -INFINITY;
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
     V3 ray_o = mk(0.0, 0.0, 0.0), ray_d = mk(0.0, 0.0, 1.0);  // next ray (state kRayReady)
@@ -127,6 +134,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         const double bound = best.kind ? best.d : INFINITY;
         if (tlo > bound + S.margin * (1.0 + fabs(bound))) return true;
         return pre.behind_ok() && thi < -S.behind_margin;
+    };
+    auto set_cull_far = [&]() {
+        const double bound = best.kind ? best.d : INFINITY;
+        const double t = bound + S.margin * (1.0 + fabs(bound));
+        float f = (float)t;
+        if ((double)f < t) f = nextafterf(f, INFINITY);
+        cull_far = f;
     };
     auto test_tri = [&](int tri) {
         if (COUNT) cnt.tri_tests++;
@@ -142,6 +156,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             best.kind = kTri;
             best.index = tri;
             best.object = cur_object;
+            set_cull_far();
         }
     };
     // next BVH (from bvh_i) with work; false when the ray is fully traced
@@ -153,7 +168,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             double lo, hi;
             if (COUNT) cnt.box_tests++;
             if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
-            if (bvh.root < 0) {
+            if (bvh.root < 0) {  // a one-triangle BVH
                 test_tri(~bvh.root);
                 continue;
             }
@@ -184,6 +199,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 best.index = i;
                 best.object = pr.object;
             }
+        }
+        set_cull_far();
+        if (pre.behind_ok()) {
+            float f = (float)(-S.behind_margin);
+            if ((double)f > -S.behind_margin) f = nextafterf(f, -INFINITY);
+            cull_behind = f;
+        } else {
+            cull_behind = -INFINITY;
         }
         bvh_i = 0;
         node = -1;
@@ -425,34 +448,48 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         do {
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             VR_STAMP(5);
-            if (state == kTraversing) {
+            // node step: lanes with room for two more pending leaves
+            if (state == kTraversing && node >= 0 && np <= 2) {
                 const Node32& nd = S.nodes32[node];
                 if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
                 const int c0 = nd.child[0], c1 = nd.child[1];
                 float f0, g0, f1, g1;
                 const int r0 = slab32(nd.box[0], pre32, f0, g0);
                 const int r1 = slab32(nd.box[1], pre32, f1, g1);
-                double lo0 = f0, hi0 = g0, lo1 = f1, hi1 = g1;
-                bool h0 = r0 == 1, h1 = r1 == 1;
+                bool h0 = r0 == 1 && !(f0 > cull_far || g0 < cull_behind);
+                bool h1 = r1 == 1 && !(f1 > cull_far || g1 < cull_behind);
                 if (r0 == 2 || r1 == 2) { VR_SEC(2); }
-                if (r0 == 2) { if (COUNT) cnt.exact_boxes++; h0 = slab(S.nodes[node].box[0], pre, lo0, hi0); }
-                if (r1 == 2) { if (COUNT) cnt.exact_boxes++; h1 = slab(S.nodes[node].box[1], pre, lo1, hi1); }
-                h0 = h0 && !culled(lo0, hi0);
-                h1 = h1 && !culled(lo1, hi1);
-                // leaf children: one inlined triangle test, run once or twice
-                int ta = -1, tb = -1;
-                if (h0 && c0 < 0) { ta = ~c0; h0 = false; }
-                if (h1 && c1 < 0) { if (ta < 0) ta = ~c1; else tb = ~c1; h1 = false; }
-                bool second = false;
-                while (ta >= 0) {
-                    if (second) { VR_SEC(1); } else { VR_SEC(0); }
-                    second = true;
-                    test_tri(ta);
-                    ta = tb;
-                    tb = -1;
+                if (r0 == 2) {  // too close to call in f32: the exact test and the f64 cull
+                    if (COUNT) cnt.exact_boxes++;
+                    double lo, hi;
+                    h0 = slab(S.nodes[node].box[0], pre, lo, hi) && !culled(lo, hi);
+                }
+                if (r1 == 2) {
+                    if (COUNT) cnt.exact_boxes++;
+                    double lo, hi;
+                    h1 = slab(S.nodes[node].box[1], pre, lo, hi) && !culled(lo, hi);
+                }
+                // leaf: queue its triangle (selects, not stores through a pointer to the slot:
+                // that would demote p0..p3 to scratch memory)
+                if (h0 && c0 < 0) {
+                    const int t = ~c0;
+                    p2 = np == 2 ? t : p2;
+                    p1 = np == 1 ? t : p1;
+                    p0 = np == 0 ? t : p0;
+                    ++np;
+                    h0 = false;
+                }
+                if (h1 && c1 < 0) {
+                    const int t = ~c1;
+                    p3 = np == 3 ? t : p3;
+                    p2 = np == 2 ? t : p2;
+                    p1 = np == 1 ? t : p1;
+                    p0 = np == 0 ? t : p0;
+                    ++np;
+                    h1 = false;
                 }
                 if (h0 && h1) {
-                    const bool swap = lo1 < lo0;  // near child first
+                    const bool swap = f1 < f0;  // near child first
                     st_node[sp * 256 + tid] = (uint32_t)(swap ? c0 : c1);
                     ++sp;
                     node = swap ? c1 : c0;
@@ -464,10 +501,31 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                     --sp;
                     node = (int)st_node[sp * 256 + tid];
                 } else {
-                    VR_SEC(8);
-                    ++bvh_i;
-                    if (!start_bvhs()) state = kTraversed;
+                    node = -1;  // this BVH is walked; its pending leaves remain
                 }
+            }
+            // leaf round: enough lanes have a pending triangle, or enough lanes (or all) are
+            // stalled on theirs
+            const uint64_t pm = __ballot(np > 0);
+            if (pm != 0) {
+                const bool stalled = np > 0 && (node < 0 || np > 2);
+                const uint64_t stm = __ballot(stalled);
+                if (__popcll(pm) >= (int)A.leaf_threshold || __popcll(stm) >= (int)A.leaf_stall ||
+                    __ballot(state == kTraversing && node >= 0 && np <= 2) == 0) {
+                    if (np > 0) {
+                        VR_SEC(0);
+                        test_tri(p0);
+                        p0 = p1;
+                        p1 = p2;
+                        p2 = p3;
+                        --np;
+                    }
+                }
+            }
+            if (state == kTraversing && node < 0 && np == 0) {
+                VR_SEC(8);
+                ++bvh_i;
+                if (!start_bvhs()) state = kTraversed;
             }
         } while (__ballot(state == kTraversing) != 0 &&
                  __popcll(__ballot(state == kTraversed)) < (int)A.shade_threshold);
