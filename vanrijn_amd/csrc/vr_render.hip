@@ -344,6 +344,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             if (COUNT && first_active_lane()) cnt.outer_slots += 64;
             VR_STAMP(5);
             if (state == kTraversed) {
+                // one call site for shade(): two inlined copies would both run whenever a wave
+                // holds camera-ray hits and bounce hits at once
+                bool go = false;
                 if (depth < 0) {
                     if (!best.kind) {
                         finish(0.0, 0.0);  // camera ray missed: photon {0, 0} (camera.rs:110-113)
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                         lambda = 380.0 + (740.0 - 380.0) * rng.standard();  // Photon::random_wavelength
                         T = 1.0; Acc = 0.0; T0 = 1.0; Acc0 = 0.0; b0 = 0.0;
                         depth = 0;
-                        shade();
+                        go = true;
                     }
                 } else if (!best.kind) {
                     finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
@@ -362,9 +365,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                         flags |= 2;
                         finish(0.0, DARK0 ? b0 : Acc0);
                     } else {
-                        shade();
+                        go = true;
                     }
                 }
+                if (go) shade();
             }
             VR_STAMP(0);
             // refill: lanes whose item is exhausted take the next items (one atomic per wave)
