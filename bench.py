@@ -141,11 +141,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms = []
+    kernel_ms, reduce_ms = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(1 + args.warmup + i, timed=True)
-        kernel_ms.append(st["kernel_ms"])
+        kernel_ms.append(st["kernel_ms"])  # render kernel only (HIP events on the launch stream)
+        reduce_ms.append(st["reduce_ms"])  # the ordered per-pixel Kahan reduce after it
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -182,6 +183,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args),
                      "kernel": "render_kernel", "kernel_ms": round(avg_kernel_s * 1e3, 3),
+                     "reduce_kernel_ms": round(sum(reduce_ms) / len(reduce_ms), 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests",
                                                                     "rays", "shaded_triangle_hits", "samples",

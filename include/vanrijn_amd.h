@@ -185,7 +185,7 @@ int vr_render_tile(const vr_scene* scene, const vr_render_params* params, vr_acc
  * weight, weight_bias} on the scene's device; `stream` is a hipStream_t (NULL = the scene's own
  * stream) and the call only enqueues work (no host synchronisation). */
 typedef struct vr_launch_stats {
-    float kernel_ms;          /* HIP-event time of the render kernel(s), valid when timed != 0 */
+    float kernel_ms;          /* HIP-event time of the render kernel launch(es), valid when timed != 0 */
     uint32_t timed;
     uint64_t box_tests;       /* filled only when counters were requested */
     uint64_t node_visits;
@@ -196,6 +196,8 @@ typedef struct vr_launch_stats {
     uint64_t traversal_slots;  /* 64 x wave-level traversal-loop iterations (lane utilisation) */
     uint64_t path_loop_slots;  /* 64 x wave-level path-loop iterations */
     uint64_t exact_box_tests;  /* f32 box tests too close to call, re-run exactly in f64 */
+    float reduce_ms;           /* HIP-event time of the ordered per-pixel Kahan reduce(s) (timed) */
+    uint32_t passes;           /* render + reduce launches (the staging buffer bounds a launch) */
 } vr_launch_stats;
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */

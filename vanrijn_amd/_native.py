@@ -87,7 +87,8 @@ class LaunchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_float), ("timed", C.c_uint32), ("box_tests", C.c_uint64),
                 ("node_visits", C.c_uint64), ("triangle_tests", C.c_uint64), ("rays", C.c_uint64),
                 ("shaded_triangle_hits", C.c_uint64), ("samples", C.c_uint64), ("traversal_slots", C.c_uint64),
-                ("path_loop_slots", C.c_uint64), ("exact_box_tests", C.c_uint64)]
+                ("path_loop_slots", C.c_uint64), ("exact_box_tests", C.c_uint64), ("reduce_ms", C.c_float),
+                ("passes", C.c_uint32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

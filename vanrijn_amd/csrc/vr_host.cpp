@@ -600,8 +600,23 @@ int vr_scene_bvh_leaf_order(const vr_scene* s, uint32_t mesh, uint64_t* out) {
 namespace {
 // Enqueue the render of params `p` into `state` on stream `st` in passes that fit the staging
 // buffer (16 B per pixel-sample: the final photon).  Caller holds s->staging_mutex.
+// Per-pass events of a timed launch: render kernel [start, mid), ordered reduce [mid, end).
+struct PassEvents {
+    std::vector<hipEvent_t> ev;
+    ~PassEvents() {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    hipEvent_t add() {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        ev.push_back(e);
+        return e;
+    }
+};
+
 int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStream_t st, bool counting,
-                   bool recording, void* records, unsigned long long* counters, unsigned long long* wg_times) {
+                   bool recording, void* records, unsigned long long* counters, unsigned long long* wg_times,
+                   PassEvents* timing = nullptr) {
     const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
     const uint64_t npix = tw * th;
     if (npix == 0 || p->spp == 0) return VR_OK;
@@ -631,9 +646,21 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;
         VR_HIP(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), st));
+        hipEvent_t mid = nullptr;
+        if (timing) {
+            hipEvent_t start = timing->add();
+            mid = timing->add();
+            if (!start || !mid) return fail(VR_ERROR_DEVICE, "hipEventCreate failed");
+            VR_HIP(hipEventRecord(start, st));
+        }
         int lr = vr::launch_render(a, stack_depth(s), counting, recording, s->dark0, s->mats ? s->mats : 3,
-                                    std::max(1, s->cu_count) * 3, st);
+                                    std::max(1, s->cu_count) * 3, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
+        if (timing) {
+            hipEvent_t end = timing->add();
+            if (!end) return fail(VR_ERROR_DEVICE, "hipEventCreate failed");
+            VR_HIP(hipEventRecord(end, st));
+        }
     }
     VR_HIP(hipEventRecord(s->staging_free, st));
     return VR_OK;
@@ -665,27 +692,28 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
             a.wg_times = (unsigned long long*)wg.ptr;
         }
     }
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (timed) {
-        VR_HIP(hipEventCreate(&e0));
-        VR_HIP(hipEventCreate(&e1));
-        VR_HIP(hipEventRecord(e0, st));
-    }
+    PassEvents pe;
     {
         std::lock_guard<std::mutex> g(ms->staging_mutex);
-        int er = enqueue_passes(ms, p, state, st, counting, false, nullptr, a.counters, a.wg_times);
+        int er = enqueue_passes(ms, p, state, st, counting, false, nullptr, a.counters, a.wg_times,
+                                timed ? &pe : nullptr);
         if (er) return er;
     }
     if (timed) {
-        VR_HIP(hipEventRecord(e1, st));
-        VR_HIP(hipEventSynchronize(e1));
-        float ms_ = 0.f;
-        VR_HIP(hipEventElapsedTime(&ms_, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        float render_ms = 0.f, reduce_ms = 0.f;
+        if (!pe.ev.empty()) VR_HIP(hipEventSynchronize(pe.ev.back()));
+        for (size_t i = 0; i + 3 <= pe.ev.size(); i += 3) {
+            float x = 0.f, y = 0.f;
+            VR_HIP(hipEventElapsedTime(&x, pe.ev[i], pe.ev[i + 1]));
+            VR_HIP(hipEventElapsedTime(&y, pe.ev[i + 1], pe.ev[i + 2]));
+            render_ms += x;
+            reduce_ms += y;
+        }
         if (stats) {
             std::memset(stats, 0, sizeof *stats);
-            stats->kernel_ms = ms_;
+            stats->kernel_ms = render_ms;
+            stats->reduce_ms = reduce_ms;
+            stats->passes = (uint32_t)(pe.ev.size() / 3);
             stats->timed = 1;
         }
         if (counting) {

@@ -151,7 +151,7 @@ enum Counter : int {
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
 int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
-                  int grid_limit, void* stream);
+                  int grid_limit, void* stream, void* mid_event = nullptr);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

@@ -8,17 +8,19 @@
 // re-association is the forward (iterative) accumulation of path throughput, which changes
 // values by O(1e-16) relative and no decision.
 //
-// Execution model (DESIGN.md "Kernel"):
-//   * one thread owns one pixel of the tile and runs its spp samples in order, so the per-pixel
-//     Kahan sums see samples in the same order as repeated update_pixel calls;
-//   * a 64-lane wave covers an 8x8 pixel block (coherent camera rays), a 256-thread workgroup a
-//     16x16 block;
-//   * each loop iteration traces exactly one ray per lane: a lane whose path ends starts its next
-//     sample's camera ray in the same iteration (path regeneration), so lanes stay busy across
-//     bounce-count divergence;
-//   * BVH traversal is a per-lane ordered stack walk over 128-B two-child nodes; the stack lives
-//     in LDS ([depth][thread], conflict-free); children are culled by the reference's exact line
-//     slab test plus a conservative distance cull (the reference has none).
+// Execution model:
+//   * persistent waves (3 per SIMD) pull single-sample work items (pixel, sample) from a global
+//     queue, 512 items per atomic into a wave-private slice (8 consecutive 8x8 pixel blocks);
+//   * each lane keeps its own path state; the wave alternates a shading phase (BSDF, next ray,
+//     end of sample + next camera ray) and a traversal phase that steps BVH nodes for every
+//     traversing lane until 56 lanes wait to shade;
+//   * traversal: per-lane ordered stack walk (LDS stack [depth][thread], node indices only) over
+//     64-B f32 nodes with outward-rounded boxes; a box test too close to call in f32 is re-run
+//     exactly in f64 on the 128-B node; leaf triangles are queued (4 per lane) and tested in f64
+//     in leaf rounds when 2 lanes stall, so the triangle test runs for many lanes at once;
+//   * each sample's final photon {wavelength, intensity} goes to a staging buffer;
+//     accumulate_kernel turns it into XYZ and folds the samples of a pixel in sample order with
+//     the reference's Kahan update_pixel, so the buffers are bit-identical to sequential calls.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -42,18 +44,16 @@ __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}
 // Render kernel: persistent waves, lane-level work queue, traversal and shading interleaved.
 //
 // Work items are (pixel, `chunk` consecutive samples), numbered chunk-major over 8x8 pixel
-// blocks.  Every lane pulls its own items (one wave-aggregated atomic per refill), so expensive
-// pixels (bunny, floor) never serialise behind a workgroup boundary: with whole 16x16 blocks x
-// 256 spp per workgroup, average workgroup concurrency was 43 % of the chip's (the most
-// expensive block alone ran 147 ms of a 293 ms launch).  Each sample's XYZ goes to a staging
-// buffer; accumulate_kernel then folds them per pixel in sample order with the reference's
-// Kahan update, so results are bit-identical to sequential update_pixel calls.
+// blocks; chunk = 1 by default (a pixel whose paths all run to the 128-bounce limit would
+// otherwise hold one lane for chunk x 128 bounces: 6.5x on the reflective bench scene).  Lanes
+// refill from a wave-private slice of the queue (`grab` items per atomic; one atomic per refill
+// cost 35 %).  With whole 16x16 blocks x 256 spp per workgroup, average workgroup concurrency
+// was 43 % of the chip's; with the queue it is 98 %.
 //
-// Inside a wave, each lane's traversal state (node, LDS stack, closest hit) stays alive across
-// iterations: the wave steps BVH nodes for all traversing lanes until at least
-// `shade_threshold` lanes have finished, then those lanes shade (BSDF, next bounce ray -- or the
-// sample's end and the next camera ray) and rejoin.  (One-ray-per-iteration lock-step measured
-// 25 % traversal lane utilisation.)  The stack holds node indices only.
+// Inside a wave, each lane's traversal state (node, LDS stack, closest hit, pending leaves)
+// stays alive across iterations: the wave steps BVH nodes for all traversing lanes until at
+// least `shade_threshold` lanes have finished, then those lanes shade and rejoin (one-ray-per-
+// iteration lock-step measured 25 % traversal lane utilisation; this scheme 58 %).
 // ----------------------------------------------------------------------------------------------
 // Items of one launch: the first spp - tail samples in chunks of `chunk`, then the last `tail`
 // samples one per item, so that a path that runs to the recursion limit near the end of the
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
 // ----------------------------------------------------------------------------------------------
 template <int STACK>
 static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int mats,
-                                  int grid_limit, hipStream_t s) {
+                                  int grid_limit, hipStream_t s, hipEvent_t mid) {
     // persistent waves: enough workgroups to fill the chip, each wave loops over work items
     const uint64_t items = dev::render_items(a, ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64);
     const uint64_t want = (items + 255) / 256;
@@ -670,6 +670,10 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
 #undef VR_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (mid) {  // between the render kernel and the ordered reduce (timed launches)
+        e = hipEventRecord(mid, s);
+        if (e != hipSuccess) return e;
+    }
     const uint64_t npix = a.tile_width * a.tile_height;
     hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
                        (const double*)a.staging, npix, a.spp, a.accumulate);
@@ -677,13 +681,14 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
 }
 
 int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int mats,
-                  int grid_limit, void* stream) {
+                  int grid_limit, void* stream, void* mid_event) {
     hipStream_t s = (hipStream_t)stream;
+    hipEvent_t mid = (hipEvent_t)mid_event;
     if (a.tile_width == 0 || a.tile_height == 0 || a.spp == 0) return 0;
     hipError_t e;
-    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, mats, grid_limit, s);
-    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, mats, grid_limit, s);
-    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, mats, grid_limit, s);
+    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, mats, grid_limit, s, mid);
+    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, mats, grid_limit, s, mid);
+    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, mats, grid_limit, s, mid);
     else return -1000;
     return (int)e;
 }
