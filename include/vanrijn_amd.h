@@ -250,6 +250,19 @@ void vr_colour_xyz_for_wavelength(double wavelength, double out[3]);
 int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, double** normals);
 void vr_mesh_free(double* vertices, double* normals);
 
+/* AccumulationBuffer::to_image_rgb_u8(&ClampingToneMapper) (accumulation_buffer.rs:38-42,
+ * image.rs:166-187, colour_xyz.rs:49-84): XYZ -> linear sRGB (the reference's matrix) ->
+ * srgb_gamma (its constants 12.98 / 1.005) -> clamp to [0, 1] -> (v * 255) truncated (NaN -> 0).
+ * vr_tone_map_device: `state` = device records (8 f64 per pixel, as vr_render_tile_device
+ * writes; colour = colour_sum * (1 / weight), 0 where weight is 0), `rgb_out` = device memory
+ * (3 bytes per pixel, row-major); enqueued on `stream` (NULL = the null stream) of `device`.
+ * vr_tone_map: host XYZ colour buffer (3 f64 per pixel) -> host RGB bytes. */
+int vr_tone_map_device(const double* state, uint64_t pixel_count, uint8_t* rgb_out, int device, void* stream);
+int vr_tone_map(const double* colour_xyz, uint64_t pixel_count, uint8_t* rgb_out, int device);
+/* ImageRgbU8::write_png (image.rs:52-66): 8-bit RGB PNG of `height` rows of `width` pixels
+ * (row 0 first).  Host only. */
+int vr_write_png(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+
 int vr_device_count(void);
 const char* vr_last_error(void);
 uint32_t vr_abi_version(void);

@@ -73,6 +73,7 @@ def lib():
             "orc_colour_xyz_to_linear_rgb": (None, [p, p]),
             "orc_colour_xyz_from_linear_rgb": (None, [p, p]),
             "orc_sky_intensity": (d, [p, d]),
+            "orc_tone_map": (None, [p, u64, p]),
             "orc_ray_for_pixel": (None, [p, u64, u64, u64, u64, d, d, p, p]),
             "orc_update_pixel": (None, [p, p, p, p, p, d, d, d]),
             "orc_merge_tile": (None, [u64, p, p, u64, u64, u64, u64, p, p]),
@@ -185,6 +186,14 @@ def xyz_for_wavelength(wl):
 def xyz_to_linear_rgb(xyz):
     out = np.zeros(3)
     lib().orc_colour_xyz_to_linear_rgb(_ptr(f64(xyz, 3)), _ptr(out))
+    return out
+
+
+def tone_map(colour):
+    """ClampingToneMapper over a colour buffer [..., 3] (XYZ) -> uint8 [..., 3]."""
+    c = np.ascontiguousarray(colour, dtype=np.float64)
+    out = np.zeros(c.shape, dtype=np.uint8)
+    lib().orc_tone_map(_ptr(c), c.size // 3, _ptr(out))
     return out
 
 

@@ -480,6 +480,27 @@ void orc_colour_xyz_from_linear_rgb(const double rgb[3], double xyz[3]) {
     st(xyz, mul_mv(&t, ld(rgb)));
 }
 
+/* colour_xyz.rs:78-84: srgb_gamma with the reference's constants (12.98, 1.005) */
+static double srgb_gamma(double u) {
+    if (u <= 0.0031308) return 12.98 * u;
+    return 1.005 * pow(u, 1.0 / 2.4) - 0.055;
+}
+/* image.rs:110-128,141-145: f64::clamp(0, 1) keeps NaN; Rust's `as u8` saturates, NaN -> 0 */
+static uint8_t clamp_to_byte(double v) {
+    if (v != v) return 0;
+    double c = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+    return (uint8_t)(c * 255.0);
+}
+/* ClampingToneMapper for ColourXyz (image.rs:166-187) over ColourXyz::to_srgb
+ * (colour_xyz.rs:69-76): colour buffer [n][3] -> RGB bytes [n][3] */
+void orc_tone_map(const double* colour, uint64_t n, uint8_t* rgb) {
+    for (uint64_t i = 0; i < n; ++i) {
+        double lin[3];
+        orc_colour_xyz_to_linear_rgb(colour + 3 * i, lin);
+        for (int k = 0; k < 3; ++k) rgb[3 * i + k] = clamp_to_byte(srgb_gamma(lin[k]));
+    }
+}
+
 /* simple_random_integrator.rs:57-65: sky = reflection_from_linear_rgb((w.y, w.y, 1)) at lambda */
 double orc_sky_intensity(const double w[3], double wl) {
     double s[32];

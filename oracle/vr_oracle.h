@@ -136,6 +136,9 @@ int orc_render_samples(const orc_scene*, uint64_t start_column, uint64_t end_col
                        uint64_t end_row, uint64_t height, uint64_t width, uint32_t spp, uint64_t seed,
                        uint64_t first_sample, int32_t mode, int32_t nthreads, orc_sample_record* out);
 
+/* AccumulationBuffer::to_image_rgb_u8(&ClampingToneMapper) on the colour buffer [n][3]. */
+void orc_tone_map(const double* colour, uint64_t n, uint8_t* rgb);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,4 +1,4 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-bash tools/gpu_check.sh || exit $?
-bash tools/pmc.sh || exit $?
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc

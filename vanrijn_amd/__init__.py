@@ -4,15 +4,15 @@ The product is the C-ABI library vanrijn_amd/lib/libvanrijn_amd.so (HIP kernels 
 include/vanrijn_amd.h).  This package is the host-side mirror of the reference's API over that
 library; every pixel is computed on the GPU.
 """
-from .render import (AccumulationBuffer, Tile, TileIterator, partial_render_scene, render_samples, render_tile,
-                     render_tile_device, resolve_state, trace_rays)
+from .render import (AccumulationBuffer, ImageRgbU8, Tile, TileIterator, partial_render_scene, render_samples,
+                     render_tile, render_tile_device, resolve_state, tone_map_device, trace_rays)
 from .scene import (BoundingVolumeHierarchy, ColourRgbF, DeviceScene, LambertianMaterial, Mesh, NamedColour, Plane,
                     ReflectiveMaterial, Scene, SceneSpec, Sphere, Spectrum, load_obj)
 from . import _native
 
 __all__ = [
-    "AccumulationBuffer", "Tile", "TileIterator", "partial_render_scene", "render_samples", "render_tile",
-    "render_tile_device", "resolve_state", "trace_rays", "BoundingVolumeHierarchy", "ColourRgbF", "DeviceScene",
+    "AccumulationBuffer", "ImageRgbU8", "Tile", "TileIterator", "partial_render_scene", "render_samples", "render_tile",
+    "render_tile_device", "resolve_state", "tone_map_device", "trace_rays", "BoundingVolumeHierarchy", "ColourRgbF", "DeviceScene",
     "LambertianMaterial", "Mesh", "NamedColour", "Plane", "ReflectiveMaterial", "Scene", "SceneSpec", "Sphere",
     "Spectrum", "load_obj",
 ]

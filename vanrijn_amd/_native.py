@@ -124,6 +124,9 @@ SIGNATURES = {
     "vr_load_obj": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.POINTER(C.c_double)),
                               C.POINTER(C.POINTER(C.c_double))]),
     "vr_mesh_free": (None, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "vr_tone_map_device": (C.c_int, [_p, _u64, _p, _i32, _p]),
+    "vr_tone_map": (C.c_int, [_p, _u64, _p, _i32]),
+    "vr_write_png": (C.c_int, [C.c_char_p, _p, _u32, _u32]),
     "vr_device_count": (C.c_int, []),
     "vr_last_error": (C.c_char_p, []),
     "vr_abi_version": (C.c_uint32, []),

@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvanrijn_amd.so")
-SOURCES = ["vr_render.hip", "vr_host.cpp"]
+SOURCES = ["vr_render.hip", "vr_image.hip", "vr_host.cpp"]
 HEADERS = ["vr_layout.h", "vr_device.h", "rgb_spectrum_tables.h", os.path.join("..", "..", "include", "vanrijn_amd.h")]
 
 FLAGS = [
@@ -44,7 +44,7 @@ def build(force=False, verbose=False):
     if not force and not stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = [hipcc()] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
+    cmd = [hipcc()] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-lz", "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -27,6 +27,8 @@
 #include "rgb_spectrum_tables.h"
 #include "vr_layout.h"
 
+#include <zlib.h>
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -967,6 +969,81 @@ int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, d
 void vr_mesh_free(double* vertices, double* normals) {
     std::free(vertices);
     std::free(normals);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Display end: ClampingToneMapper over ColourXyz::to_srgb (image.rs:166-187,
+// colour_xyz.rs:49-84) on the device, ImageRgbU8::write_png (image.rs:52-66) on the host.
+// ---------------------------------------------------------------------------------------------
+int vr_tone_map_device(const double* state, uint64_t pixel_count, uint8_t* rgb_out, int device, void* stream) {
+    if (!state || !rgb_out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    VR_HIP(hipSetDevice(device));
+    const int e = vr::launch_tonemap(state, 1, pixel_count, rgb_out, stream);
+    if (e) return fail(VR_ERROR_DEVICE, std::string("tonemap launch failed: ") + hipGetErrorString((hipError_t)e));
+    return VR_OK;
+}
+
+int vr_tone_map(const double* colour, uint64_t pixel_count, uint8_t* rgb_out, int device) {
+    if (!colour || !rgb_out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    if (pixel_count == 0) return VR_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(VR_ERROR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= n) return fail(VR_ERROR_INVALID_ARGUMENT, "device out of range");
+    VR_HIP(hipSetDevice(device));
+    CallScratch cs;
+    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    const size_t in_b = (size_t)pixel_count * 3 * sizeof(double), out_b = (size_t)pixel_count * 3;
+    VR_HIP(hipMalloc(&cs.ptr, in_b + out_b));
+    double* d_in = (double*)cs.ptr;
+    uint8_t* d_out = (uint8_t*)cs.ptr + in_b;
+    VR_HIP(hipMemcpyAsync(d_in, colour, in_b, hipMemcpyHostToDevice, cs.stream));
+    const int e = vr::launch_tonemap(d_in, 0, pixel_count, d_out, cs.stream);
+    if (e) return fail(VR_ERROR_DEVICE, std::string("tonemap launch failed: ") + hipGetErrorString((hipError_t)e));
+    VR_HIP(hipMemcpyAsync(rgb_out, d_out, out_b, hipMemcpyDeviceToHost, cs.stream));
+    VR_HIP(hipStreamSynchronize(cs.stream));
+    return VR_OK;
+}
+
+namespace {
+void png_chunk(std::vector<uint8_t>& out, const char type[4], const uint8_t* data, size_t n) {
+    const uint8_t len[4] = {(uint8_t)(n >> 24), (uint8_t)(n >> 16), (uint8_t)(n >> 8), (uint8_t)n};
+    out.insert(out.end(), len, len + 4);
+    const size_t at = out.size();
+    out.insert(out.end(), type, type + 4);
+    if (n) out.insert(out.end(), data, data + n);
+    const uLong crc = crc32(0L, out.data() + at, (uInt)(4 + n));
+    const uint8_t c[4] = {(uint8_t)(crc >> 24), (uint8_t)(crc >> 16), (uint8_t)(crc >> 8), (uint8_t)crc};
+    out.insert(out.end(), c, c + 4);
+}
+}  // namespace
+
+int vr_write_png(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height) {
+    if (!path || (!rgb && width && height)) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    if (width == 0 || height == 0) return fail(VR_ERROR_INVALID_ARGUMENT, "empty image");
+    // 8-bit RGB, no interlace; every scanline carries filter type 0 (the pixels are what the
+    // reference's png encoder stores -- its filter choice and compressed bytes may differ)
+    const size_t row = (size_t)width * 3;
+    std::vector<uint8_t> raw((row + 1) * height);
+    for (uint32_t y = 0; y < height; ++y) {
+        raw[y * (row + 1)] = 0;
+        std::memcpy(&raw[y * (row + 1) + 1], rgb + (size_t)y * row, row);
+    }
+    uLongf zn = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zn);
+    if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), 6) != Z_OK) return fail(VR_ERROR_IO, "deflate failed");
+    std::vector<uint8_t> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    const uint8_t ihdr[13] = {(uint8_t)(width >> 24), (uint8_t)(width >> 16), (uint8_t)(width >> 8), (uint8_t)width,
+                              (uint8_t)(height >> 24), (uint8_t)(height >> 16), (uint8_t)(height >> 8), (uint8_t)height,
+                              8, 2, 0, 0, 0};
+    png_chunk(out, "IHDR", ihdr, 13);
+    png_chunk(out, "IDAT", z.data(), zn);
+    png_chunk(out, "IEND", nullptr, 0);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(VR_ERROR_IO, std::string("cannot create ") + path);
+    const size_t w = std::fwrite(out.data(), 1, out.size(), f);
+    const int c = std::fclose(f);
+    if (w != out.size() || c != 0) return fail(VR_ERROR_IO, std::string("write failed: ") + path);
+    return VR_OK;
 }
 
 }  // extern "C"

@@ -152,6 +152,8 @@ enum Counter : int {
 // Launch wrappers implemented in vr_render.hip (host-callable).
 int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
                   int grid_limit, void* stream, void* mid_event = nullptr);
+// vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
+int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

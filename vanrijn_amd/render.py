@@ -3,6 +3,8 @@
     partial_render_scene(scene, tile, height, width) -> AccumulationBuffer   camera.rs:95-130
     AccumulationBuffer::{new, update_pixel, merge_tile}                     accumulation_buffer.rs:14-85
     Tile / TileIterator                                                     util/tile_iterator.rs:1-67
+    AccumulationBuffer::to_image_rgb_u8(&ClampingToneMapper)               accumulation_buffer.rs:38-42
+    ImageRgbU8 (get_colour, get_pixel_data, write_png)                      image.rs:8-66
 
 Every render call goes through the C ABI into the gfx950 kernels; nothing here computes a pixel.
 """
@@ -99,6 +101,14 @@ class AccumulationBuffer:
         dc[...] = (dc * w1 + src.colour_buffer * w2) * (1.0 / (w1 + w2))
         dw += src.weight_buffer
 
+    def to_image_rgb_u8(self, device=0) -> "ImageRgbU8":
+        """ClampingToneMapper over the XYZ colour buffer (image.rs:166-187), on the GPU."""
+        c = np.ascontiguousarray(self.colour_buffer)
+        out = np.zeros(c.shape, dtype=np.uint8)
+        N.check(N.lib().vr_tone_map(c.ctypes.data_as(C.c_void_p), c.size // 3, out.ctypes.data_as(C.c_void_p),
+                                    device))
+        return ImageRgbU8(out)
+
     @staticmethod
     def from_state(state):
         """Build from device-state records [h][w][8] = {sum XYZ, bias XYZ, weight, weight_bias}."""
@@ -187,3 +197,37 @@ def resolve_state(state):
     out = np.zeros(s.shape[:-1] + (3,))
     N.check(N.lib().vr_resolve_state(s.ctypes.data_as(C.c_void_p), s.size // 8, out.ctypes.data_as(C.c_void_p)))
     return out
+
+
+class ImageRgbU8:
+    """image.rs:8-66: 8-bit RGB pixels, row-major [height][width][3]."""
+
+    def __init__(self, data):
+        self.data = np.ascontiguousarray(data, dtype=np.uint8)
+        assert self.data.ndim == 3 and self.data.shape[2] == 3
+
+    @staticmethod
+    def new(width, height):
+        return ImageRgbU8(np.zeros((height, width, 3), dtype=np.uint8))
+
+    def get_width(self):
+        return self.data.shape[1]
+
+    def get_height(self):
+        return self.data.shape[0]
+
+    def get_colour(self, row, column):
+        return tuple(int(v) for v in self.data[row, column])
+
+    def get_pixel_data(self):
+        return self.data.tobytes()
+
+    def write_png(self, path):
+        N.check(N.lib().vr_write_png(str(path).encode(), self.data.ctypes.data_as(C.c_void_p), self.get_width(),
+                                     self.get_height()))
+
+
+def tone_map_device(state_ptr, pixel_count, rgb_ptr, stream_ptr=None, device=0):
+    """Device records (8 f64 per pixel) -> device RGB bytes (3 per pixel), enqueued on a stream."""
+    N.check(N.lib().vr_tone_map_device(C.c_void_p(state_ptr), pixel_count, C.c_void_p(rgb_ptr), device,
+                                       C.c_void_p(stream_ptr or 0)))
