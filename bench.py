@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--scene", choices=["main", "bench"], default="main")
+    ap.add_argument("--mesh", default=None,
+                    help="the reference's test_data/stanford_bunny.obj (size + sha256 verified) instead of the "
+                         "procedural stand-in")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -119,7 +122,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H, spp = args.width, args.height, args.spp
-    scene = scenes.main_scene() if args.scene == "main" else scenes.bench_scene()
+    scene = scenes.main_scene(args.mesh) if args.scene == "main" else scenes.bench_scene(args.mesh)
     dscene = scene.device_scene(local)
     info = dscene.info()
     tile = Tile(0, W, 0, H)
@@ -174,8 +177,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: procedural bunny stand-in (69,312 triangles; the reference OBJ is an LFS pointer), "
-                "counter-based RNG seed 0x5EED0001",
+        "data": ("synthetic: procedural bunny stand-in (69,312 triangles; the reference OBJ is an LFS pointer), "
+                 "counter-based RNG seed 0x5EED0001") if args.mesh is None else
+                f"{os.path.basename(args.mesh)} (sha256-verified reference bunny), counter-based RNG seed 0x5EED0001",
         "config": {"workload": f"main.rs scene (plane, 3 spheres, Lambertian bunny), {W}x{H} @{spp}spp per GPU"
                                if args.scene == "main" else f"bench scene (reflective bunny), {W}x{H} @{spp}spp per GPU",
                    "width": W, "height": H, "spp": spp, "triangles": info["triangle_count"],

@@ -882,63 +882,104 @@ int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, d
     FILE* f = std::fopen(path, "rb");
     if (!f) return fail(VR_ERROR_IO, std::string("cannot open ") + path);
     std::vector<float> pos, nrm;
+    size_t tex_count = 0;
     struct Corner {
         int64_t v, n;
     };
     std::vector<double> vout, nout;
     std::vector<Corner> poly;
-    char line[4096];
+    char* line = nullptr;
+    size_t cap = 0;
     int64_t lineno = 0;
-    auto resolve = [](int64_t idx, size_t count) -> int64_t {
-        if (idx > 0) return idx - 1;
+    // obj 0.9: 1-based indices, negative = relative to the elements read so far, 0 invalid
+    auto resolve = [](long long idx, size_t count) -> int64_t {
+        if (idx > 0) return (int64_t)idx - 1;
         if (idx < 0) return (int64_t)count + idx;
         return -1;
     };
+    auto is_space = [](char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\f' || c == '\v'; };
+    // exactly `n` f32 fields (Rust's correctly rounded str::parse::<f32>, here strtof), then an
+    // optional extra field (the w of "v x y z w") and the end of the line
+    auto floats = [&](char* e, float* out, int n, int max_fields) -> bool {
+        int got = 0;
+        while (true) {
+            while (*e && is_space(*e)) ++e;
+            if (*e == '\0' || *e == '#') break;
+            char* q;
+            const float v = std::strtof(e, &q);
+            if (q == e || (*q && !is_space(*q) && *q != '#')) return false;
+            if (got < n) out[got] = v;
+            ++got;
+            e = q;
+        }
+        return got >= n && got <= max_fields;
+    };
     int status = VR_OK;
     std::string err;
-    while (std::fgets(line, sizeof line, f)) {
+    while (getline(&line, &cap, f) != -1) {
         ++lineno;
         char* s = line;
         while (*s == ' ' || *s == '\t') ++s;
-        if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) {
-            char* e = s + 1;
-            for (int k = 0; k < 3; ++k) pos.push_back(std::strtof(e, &e));
-        } else if (s[0] == 'v' && s[1] == 'n' && (s[2] == ' ' || s[2] == '\t')) {
-            char* e = s + 2;
-            for (int k = 0; k < 3; ++k) nrm.push_back(std::strtof(e, &e));
-        } else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
+        if (s[0] == 'v' && is_space(s[1])) {
+            float xyz[3];
+            if (!floats(s + 1, xyz, 3, 4)) {
+                status = VR_ERROR_IO;
+                err = "malformed vertex at line " + std::to_string(lineno);
+                break;
+            }
+            pos.insert(pos.end(), xyz, xyz + 3);
+        } else if (s[0] == 'v' && s[1] == 'n' && is_space(s[2])) {
+            float xyz[3];
+            if (!floats(s + 2, xyz, 3, 3)) {
+                status = VR_ERROR_IO;
+                err = "malformed normal at line " + std::to_string(lineno);
+                break;
+            }
+            nrm.insert(nrm.end(), xyz, xyz + 3);
+        } else if (s[0] == 'v' && s[1] == 't' && is_space(s[2])) {
+            ++tex_count;  // texture coordinates: only counted, for index validation (mesh.rs:19)
+        } else if (s[0] == 'f' && is_space(s[1])) {
             poly.clear();
             char* e = s + 1;
             while (true) {
-                while (*e == ' ' || *e == '\t') ++e;
-                if (*e == '\0' || *e == '\n' || *e == '\r' || *e == '#') break;
+                while (*e && is_space(*e)) ++e;
+                if (*e == '\0' || *e == '#') break;
                 char* q;
-                long long vi = std::strtoll(e, &q, 10);
-                if (q == e) {
+                const long long vi = std::strtoll(e, &q, 10);
+                bool ok = q != e;
+                e = q;
+                long long ti = 0, ni = 0;
+                if (ok && *e == '/') {
+                    ++e;
+                    if (*e != '/') {
+                        ti = std::strtoll(e, &q, 10);
+                        ok = q != e;
+                        e = q;
+                    }
+                    if (ok && *e == '/') {
+                        ++e;
+                        ni = std::strtoll(e, &q, 10);
+                        ok = q != e;
+                        e = q;
+                    }
+                }
+                if (!ok || (*e && !is_space(*e) && *e != '#')) {
                     status = VR_ERROR_IO;
                     err = "malformed face at line " + std::to_string(lineno);
                     break;
                 }
-                e = q;
-                long long ni = 0;
-                if (*e == '/') {
-                    ++e;
-                    if (*e != '/') std::strtoll(e, &e, 10);  // texture index: unused (mesh.rs:19)
-                    if (*e == '/') {
-                        ++e;
-                        ni = std::strtoll(e, &e, 10);
-                    }
-                }
-                Corner c{resolve(vi, pos.size() / 3), ni ? resolve(ni, nrm.size() / 3) : -1};
-                if (c.v < 0 || (size_t)c.v >= pos.size() / 3 || (ni && (c.n < 0 || (size_t)c.n >= nrm.size() / 3))) {
+                const Corner c{resolve(vi, pos.size() / 3), ni ? resolve(ni, nrm.size() / 3) : -1};
+                const int64_t t = ti ? resolve(ti, tex_count) : 0;
+                if (c.v < 0 || (size_t)c.v >= pos.size() / 3 || (ni && (c.n < 0 || (size_t)c.n >= nrm.size() / 3)) ||
+                    (ti && (t < 0 || (size_t)t >= tex_count))) {
                     status = VR_ERROR_IO;
                     err = "face index out of range at line " + std::to_string(lineno);
                     break;
                 }
                 poly.push_back(c);
-                while (*e && *e != ' ' && *e != '\t' && *e != '\n' && *e != '\r') ++e;
             }
             if (status != VR_OK) break;
+            // get_triangles (mesh.rs:43-72): fan (v0, v_i, v_{i+1}); fewer than 3 corners: none
             for (size_t i = 1; i + 1 < poly.size(); ++i) {
                 const Corner cs3[3] = {poly[0], poly[i], poly[i + 1]};
                 for (const Corner& c : cs3) {
@@ -947,7 +988,10 @@ int vr_load_obj(const char* path, uint64_t* triangle_count, double** vertices, d
                 }
             }
         }
+        // everything else (comments, o, g, s, usemtl, mtllib, l, p, blank lines) carries no
+        // geometry for load_obj: objects and groups are flattened in file order (mesh.rs:82-85)
     }
+    std::free(line);
     std::fclose(f);
     if (status != VR_OK) return fail(status, err);
     const uint64_t n = vout.size() / 9;
