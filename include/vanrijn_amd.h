@@ -120,6 +120,10 @@ typedef struct vr_scene_desc {
 typedef struct vr_scene vr_scene;
 
 #define VR_SCENE_HOST_ONLY 1u /* build + flatten only, no device upload (inspection, CPU tests) */
+/* Build the meshes' BVHs on the device (level-synchronous sorts; the same nodes and leaf order as
+ * the host build, bounding_volume_hierarchy.rs:38-74).  Meshes with NaN coordinates use the host
+ * build.  Ignored with VR_SCENE_HOST_ONLY. */
+#define VR_SCENE_DEVICE_BVH 2u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split
@@ -139,6 +143,11 @@ typedef struct vr_scene_info {
 int vr_scene_get_info(const vr_scene* scene, vr_scene_info* out);
 /* BVH leaf (in-order) sequence of mesh `mesh`: out[i] = input triangle index of leaf i. */
 int vr_scene_bvh_leaf_order(const vr_scene* scene, uint32_t mesh, uint64_t* out);
+/* The scene's flattened BVH interior nodes (all meshes, pre-order per mesh, scene-wide links):
+ * node_count records of 128 B = { double box[2][6] (child c: min x, max x, min y, max y, min z,
+ * max z); int32 child[2] (>= 0 interior node, < 0 leaf holding triangle ~child); 24 B pad }.
+ * For inspection and build-parity tests. */
+int vr_scene_bvh_nodes(const vr_scene* scene, void* out_nodes);
 
 /* util::Tile (src/util/tile_iterator.rs:1-7): half-open row/column ranges of the full image. */
 typedef struct vr_tile {

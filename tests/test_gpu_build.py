@@ -1,0 +1,94 @@
+"""BoundingVolumeHierarchy::build_from_slice (bounding_volume_hierarchy.rs:38-74) on the device
+(VR_SCENE_DEVICE_BVH, vanrijn_amd/csrc/vr_build.hip) against the host build (vr_host.cpp), which
+the oracle pins (tests/test_oracle_scene.py: leaf orders equal to the oracle's build).
+
+Bar: identical interior nodes (child boxes compared with ==, child links), identical leaf order
+and depth, and bitwise-identical renders.  Meshes cover the shapes the median split meets: n = 1,
+2, 3 and odd sizes, equal box centres (ties broken by input index), flat axes (largest_dimension's
+-1 rule), -0.0 coordinates, and the bunny stand-in.
+"""
+import time
+
+import numpy as np
+import pytest
+
+from vanrijn_amd import scenes
+from vanrijn_amd.render import Tile, render_tile_device
+from vanrijn_amd.scene import LambertianMaterial, Mesh, Scene, Spectrum, BoundingVolumeHierarchy
+
+pytestmark = pytest.mark.gpu
+
+
+def _mesh_scene(v):
+    v = np.asarray(v, dtype=np.float64).reshape(-1, 3, 3)
+    n = np.zeros_like(v)
+    n[..., 2] = 1.0
+    mat = LambertianMaterial(Spectrum.grey(0.5), 0.5)
+    return Scene((0.0, 0.0, -5.0), [BoundingVolumeHierarchy.build(Mesh(v, n, mat))])
+
+
+def _random_mesh(rng, n, ties=False, flat=False):
+    v = rng.normal(size=(n, 3, 3))
+    if ties:  # many equal box centres
+        v = np.round(v * 2) / 2
+    if flat:  # one axis without extent
+        v[..., 2] = 0.0
+        v[: n // 3, :, 2] = -0.0
+    return v
+
+
+def _compare(scene):
+    host = scene.device_scene(0, host_only=True)
+    dev = scene.device_scene(0, device_bvh=True)
+    hi, di = host.info(), dev.info()
+    assert (hi["node_count"], hi["triangle_count"], hi["max_bvh_depth"]) == \
+           (di["node_count"], di["triangle_count"], di["max_bvh_depth"])
+    hn, dn = host.bvh_nodes(), dev.bvh_nodes()
+    assert np.array_equal(hn["child"], dn["child"])
+    assert np.array_equal(hn["box"], dn["box"])  # == : a zero's sign may differ, never a value
+    for m in range(len(scene.spec().meshes)):
+        assert np.array_equal(host.leaf_order(m), dev.leaf_order(m))
+    return dev
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 17, 1000, 4097])
+def test_device_build_matches_host_random(n):
+    rng = np.random.default_rng(n)
+    _compare(_mesh_scene(_random_mesh(rng, n)))
+
+
+@pytest.mark.parametrize("kind", ["ties", "flat"])
+def test_device_build_matches_host_degenerate(kind):
+    rng = np.random.default_rng(11)
+    _compare(_mesh_scene(_random_mesh(rng, 3000, ties=kind == "ties", flat=kind == "flat")))
+
+
+def test_device_build_bunny_renders_identically():
+    import torch
+    s = scenes.main_scene(scenes.procedural_bunny())
+    dev = _compare(s)
+    host = s.device_scene(0)
+    W, H = 192, 128
+    out = []
+    for ds in (host, dev):
+        st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
+        render_tile_device(ds, Tile(0, W, 0, H), H, W, 4, 0x5EED0001, 0, st.data_ptr())
+        out.append(st.cpu())
+    assert torch.equal(out[0], out[1])
+
+
+def test_device_build_c5_mesh():
+    """the 1,051,392-triangle synthetic mesh -- equal leaf order, and the time."""
+    v, n = scenes.synthetic_sphere_mesh()
+    s = Scene(scenes.CAMERA_LOCATION, [BoundingVolumeHierarchy.build(Mesh(v, n, LambertianMaterial(
+        Spectrum.grey(0.5), 0.5)))])
+    t0 = time.perf_counter()
+    dev = s.device_scene(0, device_bvh=True)
+    t_dev = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    host = s.device_scene(0, host_only=True)
+    t_host = time.perf_counter() - t0
+    assert np.array_equal(host.leaf_order(0), dev.leaf_order(0))
+    hn, dn = host.bvh_nodes(), dev.bvh_nodes()
+    assert np.array_equal(hn["child"], dn["child"]) and np.array_equal(hn["box"], dn["box"])
+    print(f"C5 build: device {t_dev:.3f} s, host {t_host:.3f} s")

@@ -19,6 +19,7 @@ MATERIAL_LAMBERTIAN, MATERIAL_REFLECTIVE = 0, 1
 PRIMITIVE_PLANE, PRIMITIVE_SPHERE = 0, 1
 OBJECT_PRIMITIVE_LIST, OBJECT_BVH = 0, 1
 SCENE_HOST_ONLY = 1
+SCENE_DEVICE_BVH = 2
 LAUNCH_TIMED, LAUNCH_COUNTERS = 1, 2
 
 
@@ -112,6 +113,7 @@ SIGNATURES = {
     "vr_scene_destroy": (None, [_p]),
     "vr_scene_get_info": (C.c_int, [_p, C.POINTER(SceneInfo)]),
     "vr_scene_bvh_leaf_order": (C.c_int, [_p, _u32, _p]),
+    "vr_scene_bvh_nodes": (C.c_int, [_p, _p]),
     "vr_partial_render_scene": (C.c_int, [_p, TileC, _u64, _u64, C.POINTER(AccumulationBufferC)]),
     "vr_render_tile": (C.c_int, [_p, C.POINTER(RenderParams), C.POINTER(AccumulationBufferC)]),
     "vr_render_tile_device": (C.c_int, [_p, C.POINTER(RenderParams), _p, _p, _u32, C.POINTER(LaunchStats)]),

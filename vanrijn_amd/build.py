@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvanrijn_amd.so")
-SOURCES = ["vr_render.hip", "vr_image.hip", "vr_host.cpp"]
+SOURCES = ["vr_render.hip", "vr_image.hip", "vr_build.hip", "vr_host.cpp"]
 HEADERS = ["vr_layout.h", "vr_device.h", "rgb_spectrum_tables.h", os.path.join("..", "..", "include", "vanrijn_amd.h")]
 
 FLAGS = [

@@ -1,0 +1,341 @@
+// vr_build.hip -- BoundingVolumeHierarchy::build_from_slice (bounding_volume_hierarchy.rs:38-74)
+// on the device, producing exactly the host build's flattened BVH (vr_host.cpp BvhBuilder):
+// the same pre-order node array, the same leaf order, the same child boxes.
+//
+// The reference splits every node of n > 1 triangles at n / 2 after sorting its triangles by
+// box centre along the largest extent of the node's bounds (util/axis_aligned_bounding_box.rs:
+// 76-99).  The tree's SHAPE therefore depends on n alone: a node over [lo, hi) has children
+// [lo, lo + n/2) and [lo + n/2, hi), its left child is node me + 1 and its right child node
+// me + n/2 in pre-order.  Only the split axes and the permutation depend on the geometry, so
+// the build runs level by level over the whole mesh:
+//
+//   1. bounds of every segment of the level (rocprim segmented reduce of triangle boxes,
+//      NaN-ignoring min/max like f64::min/max) -> the parent's child box and link, the axis;
+//   2. one key per position: (segment start, centre[axis] as an order-preserving u64, input
+//      index) -- positions already in leaves keep their own start as the segment;
+//   3. rocprim merge sort of the keys = every segment sorted by (centre, input index) at once
+//      (the host build breaks centre ties by input index too; pdqsort's order of equal keys is
+//      unspecified in the reference);
+//   4. the permutation follows the sorted keys.
+//
+// Work per level is O(n log n) device work; for the 1M-triangle C5 mesh the build replaces a
+// host std::sort recursion.  Scenes whose vertices contain NaN use the host build (the
+// reference's comparator maps NaN to Equal, which is not a strict order to reproduce).
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_merge_sort.hpp>
+#include <rocprim/device/device_segmented_reduce.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "vr_layout.h"
+
+namespace vr {
+namespace build {
+
+struct BoxD {
+    double mn[3], mx[3];
+};
+struct BoxUnion {  // Interval::union (interval.rs:66-77): f64::min / f64::max ignore NaN
+    __host__ __device__ BoxD operator()(const BoxD& a, const BoxD& b) const {
+        BoxD r;
+        for (int i = 0; i < 3; ++i) {
+            r.mn[i] = fmin(a.mn[i], b.mn[i]);
+            r.mx[i] = fmax(a.mx[i], b.mx[i]);
+        }
+        return r;
+    }
+};
+struct SortKey {
+    uint64_t k;     // centre[axis], order-preserving bits (-0 folded into +0: they compare equal)
+    uint32_t seg;   // start position of the segment (orders segments, keeps fixed leaves in place)
+    uint32_t orig;  // input triangle index: the tie-break
+};
+struct KeyLess {
+    __host__ __device__ bool operator()(const SortKey& a, const SortKey& b) const {
+        if (a.seg != b.seg) return a.seg < b.seg;
+        if (a.k != b.k) return a.k < b.k;
+        return a.orig < b.orig;
+    }
+};
+struct BoxOfPosition {  // position -> box of the triangle currently there
+    const BoxD* boxes;
+    const uint32_t* perm;
+    __host__ __device__ BoxD operator()(uint32_t pos) const { return boxes[perm[pos]]; }
+};
+
+__device__ __forceinline__ uint64_t order_bits(double x) {
+    if (x == 0.0) x = 0.0;
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// BoundingBox::from_points over the 3 vertices (triangle.rs:101-105) and centre() (:79-84)
+__global__ void prim_boxes_kernel(const double* verts, uint32_t n, BoxD* boxes, double* centres, uint32_t* perm) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    BoxD b;
+    for (int c = 0; c < 3; ++c) b.mn[c] = b.mx[c] = verts[9 * (uint64_t)t + c];
+    for (int k = 1; k < 3; ++k)
+        for (int c = 0; c < 3; ++c) {
+            const double v = verts[9 * (uint64_t)t + 3 * k + c];
+            b.mn[c] = fmin(b.mn[c], v);
+            b.mx[c] = fmax(b.mx[c], v);
+        }
+    boxes[t] = b;
+    for (int c = 0; c < 3; ++c) centres[3 * (uint64_t)t + c] = (b.mn[c] + b.mx[c]) / 2.0;
+    perm[t] = t;
+}
+
+// largest_dimension (util/axis_aligned_bounding_box.rs:76-99): size -1 for a flat axis, ties keep
+// the earlier axis
+__device__ __forceinline__ int largest_dimension(const BoxD& b) {
+    int acc = 0;
+    double acc_size = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const double size = b.mn[i] == b.mx[i] ? -1.0 : b.mx[i] - b.mn[i];
+        if (size > acc_size) {
+            acc = i;
+            acc_size = size;
+        }
+    }
+    return acc;
+}
+
+struct LevelSeg {
+    uint32_t lo, hi;
+    int32_t node;    // pre-order interior index within the mesh (>= 0) or -1 (a leaf)
+    int32_t parent;  // parent's interior index or -1 (the root)
+    int32_t which;   // 0 left, 1 right child of the parent
+    int32_t pad;
+};
+
+// child boxes and links into the parent; the split axis of interior segments
+__global__ void write_level_kernel(const LevelSeg* segs, uint32_t nseg, const BoxD* bounds, Node* nodes,
+                                   int32_t node_base, int32_t tri_base, int32_t* axis, double* root_box) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const LevelSeg g = segs[s];
+    const BoxD b = bounds[s];
+    double box[6];
+    for (int i = 0; i < 3; ++i) {
+        box[2 * i] = b.mn[i];
+        box[2 * i + 1] = b.mx[i];
+    }
+    if (g.parent >= 0) {
+        Node& p = nodes[g.parent];
+        for (int i = 0; i < 6; ++i) p.box[g.which][i] = box[i];
+        p.child[g.which] = g.node >= 0 ? node_base + g.node : ~(tri_base + (int32_t)g.lo);
+    } else {
+        for (int i = 0; i < 6; ++i) root_box[i] = box[i];
+    }
+    axis[s] = g.node >= 0 ? largest_dimension(b) : 0;
+}
+
+__global__ void keys_kernel(const LevelSeg* segs, uint32_t nseg, const int32_t* axis, const double* centres,
+                            const uint32_t* perm, uint32_t n, SortKey* keys) {
+    const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= n) return;
+    // the level's segments are disjoint and sorted by lo: the last one starting at or before pos
+    uint32_t a = 0, b = nseg;
+    while (b - a > 1) {
+        const uint32_t m = (a + b) / 2;
+        if (segs[m].lo <= pos) a = m;
+        else b = m;
+    }
+    const LevelSeg g = segs[a];
+    const uint32_t t = perm[pos];
+    SortKey k;
+    k.orig = t;
+    if (g.lo <= pos && pos < g.hi && g.node >= 0) {
+        k.seg = g.lo;
+        k.k = order_bits(centres[3 * (uint64_t)t + axis[a]]);
+    } else {  // a leaf (this level's or an earlier one's): stays where it is
+        k.seg = pos;
+        k.k = 0;
+    }
+    keys[pos] = k;
+}
+
+__global__ void scatter_kernel(const SortKey* keys, uint32_t n, uint32_t* perm) {
+    const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos < n) perm[pos] = keys[pos].orig;
+}
+
+// triangles and normals in leaf order
+__global__ void gather_kernel(const double* verts, const double* norms, const uint32_t* perm, uint32_t n,
+                              TriVerts* tris, TriNormals* normals) {
+    const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= n) return;
+    const uint64_t t = perm[pos];
+    TriVerts tv;
+    TriNormals tn;
+    for (int i = 0; i < 9; ++i) {
+        tv.v[i] = verts[9 * t + i];
+        tn.n[i] = norms[9 * t + i];
+    }
+    tv.pad = 0.0;
+    tn.pad = 0.0;
+    tris[pos] = tv;
+    normals[pos] = tn;
+}
+
+// the f32 traversal copy: min bounds rounded toward -inf, max bounds toward +inf (the host
+// build's nextafter rule)
+__global__ void round_nodes_kernel(const Node* nodes, uint64_t n, Node32* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Node nd = nodes[i];
+    Node32 m;
+    for (int c = 0; c < 2; ++c) {
+        for (int k = 0; k < 6; ++k) m.box[c][k] = (k & 1) ? __double2float_ru(nd.box[c][k]) : __double2float_rd(nd.box[c][k]);
+        m.child[c] = nd.child[c];
+    }
+    m.pad[0] = m.pad[1] = 0;
+    out[i] = m;
+}
+
+}  // namespace build
+
+#define VRB(call)                                 \
+    do {                                          \
+        hipError_t e_ = (call);                   \
+        if (e_ != hipSuccess) return (int)e_;     \
+    } while (0)
+
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 1); }
+};
+}  // namespace
+
+// Builds one mesh's BVH into the scene's device arrays.  verts / norms: host [n][3][3] f64.
+// nodes: the mesh's n - 1 interior nodes (pre-order, node_base-relative links made global);
+// tris / normals: its n triangles in leaf order; leaf_order (host): input index per leaf;
+// root_box (host, 6 f64); levels (host): tree depth.  Returns a hipError_t (0 = success).
+int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
+                     Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
+                     int* levels, void* stream) {
+    using namespace build;
+    hipStream_t st = (hipStream_t)stream;
+    // the tree's shape (depends on n only), level by level in pre-order
+    std::vector<std::vector<LevelSeg>> lv;
+    {
+        std::vector<LevelSeg> cur = {{0, n, n > 1 ? 0 : -1, -1, 0, 0}};
+        while (!cur.empty()) {
+            std::vector<LevelSeg> next;
+            for (const LevelSeg& g : cur) {
+                if (g.node < 0) continue;
+                const uint32_t size = g.hi - g.lo, half = size / 2, mid = g.lo + half;
+                next.push_back({g.lo, mid, half > 1 ? g.node + 1 : -1, g.node, 0, 0});
+                next.push_back({mid, g.hi, size - half > 1 ? g.node + (int32_t)half : -1, g.node, 1, 0});
+            }
+            lv.push_back(std::move(cur));
+            cur = std::move(next);
+        }
+    }
+    *levels = (int)lv.size();
+    size_t max_seg = 1;
+    for (auto& l : lv) max_seg = std::max(max_seg, l.size());
+
+    DevBuf d_verts, d_norms, d_boxes, d_centres, d_perm, d_keys, d_keys2, d_segs, d_lo, d_hi, d_bounds, d_axis,
+        d_root, d_temp;
+    VRB(d_verts.alloc(sizeof(double) * 9 * (size_t)n));
+    VRB(d_norms.alloc(sizeof(double) * 9 * (size_t)n));
+    VRB(d_boxes.alloc(sizeof(BoxD) * (size_t)n));
+    VRB(d_centres.alloc(sizeof(double) * 3 * (size_t)n));
+    VRB(d_perm.alloc(sizeof(uint32_t) * (size_t)n));
+    VRB(d_keys.alloc(sizeof(SortKey) * (size_t)n));
+    VRB(d_keys2.alloc(sizeof(SortKey) * (size_t)n));
+    VRB(d_segs.alloc(sizeof(LevelSeg) * max_seg));
+    VRB(d_lo.alloc(sizeof(uint32_t) * max_seg));
+    VRB(d_hi.alloc(sizeof(uint32_t) * max_seg));
+    VRB(d_bounds.alloc(sizeof(BoxD) * max_seg));
+    VRB(d_axis.alloc(sizeof(int32_t) * max_seg));
+    VRB(d_root.alloc(sizeof(double) * 6));
+    VRB(hipMemcpyAsync(d_verts.p, verts, sizeof(double) * 9 * (size_t)n, hipMemcpyHostToDevice, st));
+    VRB(hipMemcpyAsync(d_norms.p, norms, sizeof(double) * 9 * (size_t)n, hipMemcpyHostToDevice, st));
+    const dim3 blk(256);
+    auto grid = [](uint64_t m) { return dim3((unsigned)((m + 255) / 256)); };
+    BoxD* boxes = (BoxD*)d_boxes.p;
+    uint32_t* perm = (uint32_t*)d_perm.p;
+    SortKey* keys = (SortKey*)d_keys.p;
+    SortKey* keys2 = (SortKey*)d_keys2.p;
+    hipLaunchKernelGGL(prim_boxes_kernel, grid(n), blk, 0, st, (const double*)d_verts.p, n, boxes,
+                       (double*)d_centres.p, perm);
+    VRB(hipGetLastError());
+
+    // temporary storage: the largest of the two primitives' needs
+    auto box_in = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0),
+                                                   BoxOfPosition{boxes, perm});
+    BoxD empty;
+    for (int i = 0; i < 3; ++i) {
+        empty.mn[i] = INFINITY;
+        empty.mx[i] = -INFINITY;
+    }
+    size_t t_red = 0, t_sort = 0;
+    VRB(rocprim::segmented_reduce(nullptr, t_red, box_in, (BoxD*)d_bounds.p, (unsigned)max_seg, (uint32_t*)d_lo.p,
+                                  (uint32_t*)d_hi.p, BoxUnion{}, empty, st));
+    VRB(rocprim::merge_sort(nullptr, t_sort, keys, keys2, (size_t)n, KeyLess{}, st));
+    VRB(d_temp.alloc(std::max(t_red, t_sort)));
+
+    std::vector<uint32_t> lo, hi;
+    for (size_t L = 0; L < lv.size(); ++L) {
+        const std::vector<LevelSeg>& segs = lv[L];
+        const uint32_t ns = (uint32_t)segs.size();
+        lo.resize(ns);
+        hi.resize(ns);
+        bool interior = false;
+        for (uint32_t i = 0; i < ns; ++i) {
+            lo[i] = segs[i].lo;
+            hi[i] = segs[i].hi;
+            interior = interior || segs[i].node >= 0;
+        }
+        VRB(hipMemcpyAsync(d_segs.p, segs.data(), sizeof(LevelSeg) * ns, hipMemcpyHostToDevice, st));
+        VRB(hipMemcpyAsync(d_lo.p, lo.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
+        VRB(hipMemcpyAsync(d_hi.p, hi.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
+        size_t tb = t_red;
+        VRB(rocprim::segmented_reduce(d_temp.p, tb, box_in, (BoxD*)d_bounds.p, ns, (uint32_t*)d_lo.p,
+                                      (uint32_t*)d_hi.p, BoxUnion{}, empty, st));
+        hipLaunchKernelGGL(write_level_kernel, grid(ns), blk, 0, st, (const LevelSeg*)d_segs.p, ns,
+                           (const BoxD*)d_bounds.p, nodes, node_base, tri_base, (int32_t*)d_axis.p,
+                           (double*)d_root.p);
+        VRB(hipGetLastError());
+        if (!interior) continue;
+        hipLaunchKernelGGL(keys_kernel, grid(n), blk, 0, st, (const LevelSeg*)d_segs.p, ns,
+                           (const int32_t*)d_axis.p, (const double*)d_centres.p, (const uint32_t*)perm, n, keys);
+        VRB(hipGetLastError());
+        tb = t_sort;
+        VRB(rocprim::merge_sort(d_temp.p, tb, keys, keys2, (size_t)n, KeyLess{}, st));
+        hipLaunchKernelGGL(scatter_kernel, grid(n), blk, 0, st, (const SortKey*)keys2, n, perm);
+        VRB(hipGetLastError());
+    }
+    hipLaunchKernelGGL(gather_kernel, grid(n), blk, 0, st, (const double*)d_verts.p, (const double*)d_norms.p,
+                       (const uint32_t*)perm, n, tris, normals);
+    VRB(hipGetLastError());
+    std::vector<uint32_t> p(n);
+    VRB(hipMemcpyAsync(p.data(), perm, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, st));
+    VRB(hipMemcpyAsync(root_box, d_root.p, sizeof(double) * 6, hipMemcpyDeviceToHost, st));
+    VRB(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n; ++i) leaf_order[i] = p[i];
+    return 0;
+}
+
+int device_round_nodes(const Node* nodes, uint64_t n, Node32* out, void* stream) {
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(build::round_nodes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, n,
+                       out);
+    return (int)hipGetLastError();
+}
+
+}  // namespace vr

@@ -172,6 +172,18 @@ struct vr_scene {
     std::vector<int> mesh_tri_base;
     int max_depth = 0;
     uint32_t object_count = 0;
+    // VR_SCENE_DEVICE_BVH: the meshes' BVHs are built on the device after upload (host vectors
+    // nodes / nodes32 / tris / normals stay empty; the counts below size the device arrays)
+    bool device_bvh = false;
+    uint64_t node_count = 0, tri_count = 0;
+    struct PendingMesh {
+        const double* vertices;
+        const double* normals;
+        uint64_t n;
+        int32_t node_base, tri_base;
+        uint32_t mesh;
+    };
+    std::vector<PendingMesh> pending;
     bool dark0 = true;  // every material's colour(0 nm) == 0: the recursion-limit photon needs no lambda-0 chain
     int mats = 0;       // bit 0: a Lambertian material exists, bit 1: a reflective one
     // device copies
@@ -202,12 +214,21 @@ size_t align_up(size_t v) {
     return (v + 255) & ~size_t(255);
 }
 
+struct CallScratch {
+    hipStream_t stream = nullptr;
+    void* ptr = nullptr;
+    ~CallScratch() {
+        if (ptr) (void)hipFree(ptr);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
 int upload(vr_scene* s) {
     VR_HIP(hipSetDevice(s->device));
-    const size_t sz_nodes = s->nodes.size() * sizeof(vr::Node);
-    const size_t sz_nodes32 = s->nodes32.size() * sizeof(vr::Node32);
-    const size_t sz_tris = s->tris.size() * sizeof(vr::TriVerts);
-    const size_t sz_norm = s->normals.size() * sizeof(vr::TriNormals);
+    const size_t sz_nodes = s->node_count * sizeof(vr::Node);
+    const size_t sz_nodes32 = s->node_count * sizeof(vr::Node32);
+    const size_t sz_tris = s->tri_count * sizeof(vr::TriVerts);
+    const size_t sz_norm = s->tri_count * sizeof(vr::TriNormals);
     const size_t sz_mat = s->materials.size() * sizeof(vr::Material);
     const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
     const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
@@ -226,10 +247,13 @@ int upload(vr_scene* s) {
     char* base = (char*)s->d_block;
     const void* src[6] = {s->nodes.data(), s->tris.data(), s->normals.data(), s->materials.data(), s->prims.data(),
                           s->bvhs.data()};
-    for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 6; ++i) {
+        if (s->device_bvh && i < 3) continue;  // filled by the device build below
         if (sizes[i]) VR_HIP(hipMemcpy(base + off[i], src[i], sizes[i], hipMemcpyHostToDevice));
+    }
     VR_HIP(hipMemset(base + off[6], 0, sizes[6]));
-    if (sz_nodes32) VR_HIP(hipMemcpy(base + off[7], s->nodes32.data(), sz_nodes32, hipMemcpyHostToDevice));
+    if (sz_nodes32 && !s->device_bvh)
+        VR_HIP(hipMemcpy(base + off[7], s->nodes32.data(), sz_nodes32, hipMemcpyHostToDevice));
     s->d_error = (int32_t*)(base + off[6]);
     s->d_counters = (unsigned long long*)(base + off[6] + 64);
     vr::DeviceScene& d = s->dev;
@@ -240,6 +264,27 @@ int upload(vr_scene* s) {
     d.materials = (const vr::Material*)(base + off[3]);
     d.prims = (const vr::Prim*)(base + off[4]);
     d.bvhs = (const vr::Bvh*)(base + off[5]);
+    if (s->device_bvh) {
+        // BoundingVolumeHierarchy::build on the device (vr_build.hip): same nodes, same leaf order
+        CallScratch cs;
+        VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+        vr::Node* nodes = (vr::Node*)(base + off[0]);
+        for (const auto& pm : s->pending) {
+            double root_box[6];
+            int levels = 0;
+            const int e = vr::device_build_bvh(pm.vertices, pm.normals, (uint32_t)pm.n, pm.node_base, pm.tri_base,
+                                               nodes + pm.node_base, (vr::TriVerts*)(base + off[1]) + pm.tri_base,
+                                               (vr::TriNormals*)(base + off[2]) + pm.tri_base,
+                                               s->leaf_order[pm.mesh].data(), root_box, &levels, cs.stream);
+            if (e) return fail(VR_ERROR_DEVICE, std::string("device BVH build failed: ") +
+                                                    hipGetErrorString((hipError_t)e));
+            s->max_depth = std::max(s->max_depth, levels);
+        }
+        const int e = vr::device_round_nodes(nodes, s->node_count, (vr::Node32*)(base + off[7]), cs.stream);
+        if (e) return fail(VR_ERROR_DEVICE, "device node rounding failed");
+        VR_HIP(hipStreamSynchronize(cs.stream));
+        s->pending.clear();  // the caller's arrays are not kept
+    }
     return VR_OK;
 }
 
@@ -317,14 +362,6 @@ int read_and_clear_error(const vr_scene* s, hipStream_t stream) {
 }
 
 // RAII device buffer + stream for the synchronous host-buffer entry points
-struct CallScratch {
-    hipStream_t stream = nullptr;
-    void* ptr = nullptr;
-    ~CallScratch() {
-        if (ptr) (void)hipFree(ptr);
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-};
 
 }  // namespace
 
@@ -470,11 +507,56 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     s->object_count = desc->object_count;
     s->leaf_order.resize(desc->mesh_count);
     s->mesh_tri_base.assign(desc->mesh_count, 0);
+    // device build: requested, a device exists for it, and no NaN coordinate (the reference's
+    // sort comparator maps NaN to Equal, which only the host build reproduces)
+    s->device_bvh = (flags & VR_SCENE_DEVICE_BVH) != 0 && !s->host_only;
+    for (uint32_t mi = 0; s->device_bvh && mi < desc->mesh_count; ++mi) {
+        const vr_mesh_desc& m = desc->meshes[mi];
+        if (m.triangle_count && !m.vertices) break;
+        for (uint64_t i = 0; i < 9 * m.triangle_count; ++i)
+            if (m.vertices[i] != m.vertices[i]) {
+                s->device_bvh = false;
+                break;
+            }
+    }
     for (uint32_t mi = 0; mi < desc->mesh_count; ++mi) {
         const vr_mesh_desc& m = desc->meshes[mi];
         if (m.triangle_count && (!m.vertices || !m.normals)) return bad("mesh without vertex or normal arrays");
         if (m.material >= desc->material_count) return bad("mesh material out of range");
-        if (s->tris.size() + m.triangle_count > (uint64_t)INT32_MAX) return bad("too many triangles (2^31)");
+        if (s->tri_count + m.triangle_count > (uint64_t)INT32_MAX) return bad("too many triangles (2^31)");
+        if (s->device_bvh) {
+            // shape and root box on the host (O(n)); the sort-based build runs after upload
+            vr::Bvh bvh{};
+            bvh.object = mesh_object[mi];
+            bvh.tri_base = (int32_t)s->tri_count;
+            bvh.material = (int32_t)m.material;
+            s->mesh_tri_base[mi] = bvh.tri_base;
+            Box3 rb = box_empty();
+            for (uint64_t t = 0; t < m.triangle_count; ++t) {
+                Box3 bb = box_empty();
+                for (int k = 0; k < 3; ++k)
+                    for (int c = 0; c < 3; ++c) {
+                        const double v = m.vertices[9 * t + 3 * k + c];
+                        bb.b[c] = iv_expand(bb.b[c], v);
+                        extent = std::max(extent, std::fabs(v));
+                    }
+                rb = box_union(rb, bb);
+            }
+            if (m.triangle_count == 0) {
+                bvh.root = INT32_MIN;
+                for (int i = 0; i < 6; ++i) bvh.root_box[i] = (i & 1) ? -INFINITY : INFINITY;
+            } else {
+                box_to_layout(rb, bvh.root_box);
+                bvh.root = m.triangle_count > 1 ? (int32_t)s->node_count : ~bvh.tri_base;
+                s->pending.push_back({m.vertices, m.normals, m.triangle_count, (int32_t)s->node_count, bvh.tri_base, mi});
+                s->max_depth = std::max(s->max_depth, 1);
+            }
+            s->leaf_order[mi].assign(m.triangle_count, 0);
+            s->node_count += m.triangle_count ? m.triangle_count - 1 : 0;
+            s->tri_count += m.triangle_count;
+            if (mesh_object[mi] >= 0) s->bvhs.push_back(bvh);
+            continue;
+        }
         BvhBuilder B;
         B.tri_base = (int)s->tris.size();
         s->mesh_tri_base[mi] = B.tri_base;
@@ -524,6 +606,8 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
             s->normals.push_back(tn);
         }
         if (mesh_object[mi] >= 0) s->bvhs.push_back(bvh);
+        s->node_count = s->nodes.size();
+        s->tri_count = s->tris.size();
     }
     // BVH objects in object order (ties across objects depend on it)
     std::sort(s->bvhs.begin(), s->bvhs.end(), [](const vr::Bvh& a, const vr::Bvh& b) { return a.object < b.object; });
@@ -584,12 +668,25 @@ void vr_scene_destroy(vr_scene* s) {
 
 int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     if (!s || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
-    out->triangle_count = s->tris.size();
-    out->node_count = s->nodes.size();
+    out->triangle_count = s->tri_count;
+    out->node_count = s->node_count;
     out->max_bvh_depth = (uint32_t)s->max_depth;
     out->object_count = s->object_count;
     out->extent = s->extent;
     out->device_bytes = s->device_bytes;
+    return VR_OK;
+}
+
+int vr_scene_bvh_nodes(const vr_scene* s, void* out) {
+    if (!s || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    const size_t bytes = s->node_count * sizeof(vr::Node);
+    if (bytes == 0) return VR_OK;
+    if (!s->device_bvh) {
+        std::memcpy(out, s->nodes.data(), bytes);
+        return VR_OK;
+    }
+    VR_HIP(hipSetDevice(s->device));
+    VR_HIP(hipMemcpy(out, s->dev.nodes, bytes, hipMemcpyDeviceToHost));
     return VR_OK;
 }
 

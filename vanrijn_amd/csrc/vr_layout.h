@@ -154,6 +154,11 @@ int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool r
                   int grid_limit, void* stream, void* mid_event = nullptr);
 // vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
+// vr_build.hip: one mesh's BVH on the device (same nodes and leaf order as the host build)
+int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
+                     Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
+                     int* levels, void* stream);
+int device_round_nodes(const Node* nodes, uint64_t n, Node32* out, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

@@ -248,17 +248,18 @@ class Scene:
             self._spec = SceneSpec(self.camera_location, mats, meshes, objs)
         return self._spec
 
-    def device_scene(self, device=0, host_only=False):
-        key = (device, host_only)
+    def device_scene(self, device=0, host_only=False, device_bvh=False):
+        key = (device, host_only, device_bvh)
         if key not in self._device_scenes:
-            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only)
+            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh)
         return self._device_scenes[key]
 
 
 class DeviceScene:
     """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
 
-    def __init__(self, spec: SceneSpec, device=0, host_only=False):
+    def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False):
+        """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH; same nodes and leaf order)."""
         L = N.lib()
         self.spec = spec
         keep = []  # keep ctypes buffers alive during vr_scene_create
@@ -290,7 +291,8 @@ class DeviceScene:
         desc = N.SceneDesc(N.Vec3(*spec.camera_location), len(spec.materials), len(prims), len(meshes), len(objs),
                            mats, prim_arr, mesh_arr, obj_arr)
         h = C.c_void_p()
-        N.check(L.vr_scene_create(C.byref(desc), device, N.SCENE_HOST_ONLY if host_only else 0, C.byref(h)))
+        flags = (N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0)
+        N.check(L.vr_scene_create(C.byref(desc), device, flags, C.byref(h)))
         self.handle = h
         self.device = device
         self.host_only = host_only
@@ -305,6 +307,15 @@ class DeviceScene:
         i = N.SceneInfo()
         N.check(N.lib().vr_scene_get_info(self.handle, C.byref(i)))
         return {n: getattr(i, n) for n, _ in i._fields_}
+
+    NODE_DTYPE = np.dtype([("box", "<f8", (2, 6)), ("child", "<i4", (2,)), ("pad", "<i4", (6,))])
+
+    def bvh_nodes(self):
+        """The flattened interior nodes (vr_scene_bvh_nodes), a structured array."""
+        out = np.zeros(self.info()["node_count"], dtype=self.NODE_DTYPE)
+        if out.size:
+            N.check(N.lib().vr_scene_bvh_nodes(self.handle, out.ctypes.data_as(C.c_void_p)))
+        return out
 
     def leaf_order(self, mesh):
         out = np.zeros(len(self.spec.meshes[mesh].vertices), dtype=np.uint64)
