@@ -124,6 +124,10 @@ typedef struct vr_scene vr_scene;
  * the host build, bounding_volume_hierarchy.rs:38-74).  Meshes with NaN coordinates use the host
  * build.  Ignored with VR_SCENE_HOST_ONLY. */
 #define VR_SCENE_DEVICE_BVH 2u
+/* Traverse the reference's own median-split tree instead of the default SAH tree.  Results are
+ * identical either way (the closest hit does not depend on the tree; ties follow the reference
+ * tree's in-order leaf rank); the device build always produces the reference tree. */
+#define VR_SCENE_REFERENCE_BVH 4u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split

@@ -38,7 +38,7 @@ def _random_mesh(rng, n, ties=False, flat=False):
 
 
 def _compare(scene):
-    host = scene.device_scene(0, host_only=True)
+    host = scene.device_scene(0, host_only=True, reference_bvh=True)
     dev = scene.device_scene(0, device_bvh=True)
     hi, di = host.info(), dev.info()
     assert (hi["node_count"], hi["triangle_count"], hi["max_bvh_depth"]) == \
@@ -67,14 +67,16 @@ def test_device_build_bunny_renders_identically():
     import torch
     s = scenes.main_scene(scenes.procedural_bunny())
     dev = _compare(s)
-    host = s.device_scene(0)
+    host = s.device_scene(0, reference_bvh=True)
+    sah = s.device_scene(0)  # the default SAH traversal tree: the same image, bit for bit
     W, H = 192, 128
     out = []
-    for ds in (host, dev):
+    for ds in (host, dev, sah):
         st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
         render_tile_device(ds, Tile(0, W, 0, H), H, W, 4, 0x5EED0001, 0, st.data_ptr())
         out.append(st.cpu())
     assert torch.equal(out[0], out[1])
+    assert torch.equal(out[0], out[2])
 
 
 def test_device_build_c5_mesh():
@@ -86,7 +88,7 @@ def test_device_build_c5_mesh():
     dev = s.device_scene(0, device_bvh=True)
     t_dev = time.perf_counter() - t0
     t0 = time.perf_counter()
-    host = s.device_scene(0, host_only=True)
+    host = s.device_scene(0, host_only=True, reference_bvh=True)
     t_host = time.perf_counter() - t0
     assert np.array_equal(host.leaf_order(0), dev.leaf_order(0))
     hn, dn = host.bvh_nodes(), dev.bvh_nodes()

@@ -35,11 +35,16 @@ def test_procedural_bunny_is_deterministic(bunny):
 def test_bvh_leaf_order_matches_oracle(oracle, bunny):
     for scene in (scenes.main_scene(bunny), scenes.bench_scene(bunny)):
         spec = scene.spec()
-        ds = scene.device_scene(0, host_only=True)
         orc = oracle.OracleScene(spec)
         obj = [i for i, o in enumerate(spec.objects) if o.kind == "bvh"][0]
-        assert np.array_equal(ds.leaf_order(0).astype(np.int64), orc.leaf_order(obj))
-        assert ds.info()["max_bvh_depth"] == orc.depth(obj)
+        # the reference tree's in-order leaves (the tie-break ranks) with either traversal tree
+        for reference_bvh in (True, False):
+            ds = scene.device_scene(0, host_only=True, reference_bvh=reference_bvh)
+            assert np.array_equal(ds.leaf_order(0).astype(np.int64), orc.leaf_order(obj))
+        ref = scene.device_scene(0, host_only=True, reference_bvh=True)
+        assert ref.info()["max_bvh_depth"] == orc.depth(obj)
+        nodes = ref.bvh_nodes()
+        assert len(nodes) == len(bunny[0]) - 1
 
 
 def test_spectrum_helpers_match_oracle(oracle):

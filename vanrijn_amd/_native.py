@@ -20,6 +20,7 @@ PRIMITIVE_PLANE, PRIMITIVE_SPHERE = 0, 1
 OBJECT_PRIMITIVE_LIST, OBJECT_BVH = 0, 1
 SCENE_HOST_ONLY = 1
 SCENE_DEVICE_BVH = 2
+SCENE_REFERENCE_BVH = 4
 LAUNCH_TIMED, LAUNCH_COUNTERS = 1, 2
 
 

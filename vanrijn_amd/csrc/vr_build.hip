@@ -169,7 +169,7 @@ __global__ void scatter_kernel(const SortKey* keys, uint32_t n, uint32_t* perm) 
 
 // triangles and normals in leaf order
 __global__ void gather_kernel(const double* verts, const double* norms, const uint32_t* perm, uint32_t n,
-                              TriVerts* tris, TriNormals* normals) {
+                              int32_t tri_base, TriVerts* tris, TriNormals* normals) {
     const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
     if (pos >= n) return;
     const uint64_t t = perm[pos];
@@ -179,7 +179,7 @@ __global__ void gather_kernel(const double* verts, const double* norms, const ui
         tv.v[i] = verts[9 * t + i];
         tn.n[i] = norms[9 * t + i];
     }
-    tv.pad = 0.0;
+    tv.rank = tri_base + (int64_t)pos;  // this build IS the reference topology
     tn.pad = 0.0;
     tris[pos] = tv;
     normals[pos] = tn;
@@ -320,7 +320,7 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
         VRB(hipGetLastError());
     }
     hipLaunchKernelGGL(gather_kernel, grid(n), blk, 0, st, (const double*)d_verts.p, (const double*)d_norms.p,
-                       (const uint32_t*)perm, n, tris, normals);
+                       (const uint32_t*)perm, n, tri_base, tris, normals);
     VRB(hipGetLastError());
     std::vector<uint32_t> p(n);
     VRB(hipMemcpyAsync(p.data(), perm, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, st));

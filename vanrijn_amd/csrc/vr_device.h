@@ -441,7 +441,8 @@ __device__ __forceinline__ void traverse_bvh(const DeviceScene& S, const Bvh& bv
         if (d < 0.0) return;
         bool take;
         if (!best.kind || d < best.d) take = true;
-        else if (d == best.d) take = (best.object == bvh.object) ? (tri > best.index) : (bvh.object < best.object);
+        else if (d == best.d)
+            take = (best.object == bvh.object) ? (S.tris[tri].rank > S.tris[best.index].rank) : (bvh.object < best.object);
         else take = false;
         if (take) {
             best.d = d;

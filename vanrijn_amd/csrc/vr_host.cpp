@@ -151,6 +151,123 @@ struct BvhBuilder {
     }
 };
 
+// Traversal tree (the default): a binned-SAH binary tree over the same triangles, leaf size 1.
+// The reference's closest hit does not depend on its tree: a box test on a superset box passes
+// whenever it passes on the subset (every rounding step of (bound - o) / d is monotonic in
+// `bound`), so a triangle is reachable in the reference tree iff the exact line test passes on
+// its OWN box -- which this tree tests too, as the leaf child's box -- and distance ties are
+// broken by the reference in-order rank carried in TriVerts::rank.  Only the amount of work
+// depends on the tree: SAH splits cut node visits against the median split.
+struct SahBuilder {
+    std::vector<BuildPrim>& prims;  // permuted in place into this tree's leaf order
+    std::vector<vr::Node> nodes;
+    int max_depth = 0;
+    int tri_base = 0;
+    explicit SahBuilder(std::vector<BuildPrim>& p) : prims(p) {}
+
+    static double area(const Box3& b) {
+        const double dx = b.b[0].max - b.b[0].min, dy = b.b[1].max - b.b[1].min, dz = b.b[2].max - b.b[2].min;
+        if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+
+    uint64_t split(uint64_t lo, uint64_t hi, int level) {
+        const uint64_t n = hi - lo;
+        double cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint64_t i = lo; i < hi; ++i)
+            for (int c = 0; c < 3; ++c) {
+                cmin[c] = std::min(cmin[c], prims[i].centre[c]);
+                cmax[c] = std::max(cmax[c], prims[i].centre[c]);
+            }
+        constexpr int kBins = 32;
+        int best_axis = -1, best_bin = -1;
+        double best_cost = INFINITY;
+        // median splits where SAH would push the tree past the deepest traversal stack (48)
+        const int need = n > 1 ? 64 - __builtin_clzll(n - 1) : 0;  // ceil(log2 n)
+        if (level + need < 44) {
+            for (int a = 0; a < 3; ++a) {
+                const double ext = cmax[a] - cmin[a];
+                if (!(ext > 0.0)) continue;
+                Box3 bb[kBins];
+                uint64_t cnt[kBins] = {};
+                for (int k = 0; k < kBins; ++k) bb[k] = box_empty();
+                const double scale = kBins / ext;
+                for (uint64_t i = lo; i < hi; ++i) {
+                    int k = (int)((prims[i].centre[a] - cmin[a]) * scale);
+                    k = std::min(kBins - 1, std::max(0, k));
+                    ++cnt[k];
+                    bb[k] = box_union(bb[k], prims[i].box);
+                }
+                double right_area[kBins];
+                uint64_t right_cnt[kBins];
+                Box3 acc = box_empty();
+                uint64_t c = 0;
+                for (int k = kBins - 1; k > 0; --k) {
+                    acc = box_union(acc, bb[k]);
+                    c += cnt[k];
+                    right_area[k] = area(acc);
+                    right_cnt[k] = c;
+                }
+                acc = box_empty();
+                c = 0;
+                for (int k = 0; k < kBins - 1; ++k) {
+                    acc = box_union(acc, bb[k]);
+                    c += cnt[k];
+                    if (c == 0 || right_cnt[k + 1] == 0) continue;
+                    const double cost = area(acc) * (double)c + right_area[k + 1] * (double)right_cnt[k + 1];
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        best_axis = a;
+                        best_bin = k;
+                    }
+                }
+            }
+        }
+        if (best_axis >= 0) {
+            const double ext = cmax[best_axis] - cmin[best_axis], scale = kBins / ext;
+            auto mid = std::partition(prims.begin() + lo, prims.begin() + hi, [&](const BuildPrim& p) {
+                int k = (int)((p.centre[best_axis] - cmin[best_axis]) * scale);
+                k = std::min(kBins - 1, std::max(0, k));
+                return k <= best_bin;
+            });
+            const uint64_t m = (uint64_t)(mid - prims.begin());
+            if (m > lo && m < hi) return m;
+        }
+        // median split on the widest centroid axis (ties by reference rank: deterministic)
+        int a = 0;
+        for (int c = 1; c < 3; ++c)
+            if (cmax[c] - cmin[c] > cmax[a] - cmin[a]) a = c;
+        const uint64_t m = lo + n / 2;
+        std::nth_element(prims.begin() + lo, prims.begin() + m, prims.begin() + hi,
+                         [a](const BuildPrim& x, const BuildPrim& y) {
+                             if (x.centre[a] < y.centre[a]) return true;
+                             if (x.centre[a] > y.centre[a]) return false;
+                             return x.orig < y.orig;
+                         });
+        return m;
+    }
+
+    int32_t build(uint64_t lo, uint64_t hi, int level, Box3& bounds) {
+        max_depth = std::max(max_depth, level + 1);
+        bounds = box_empty();
+        for (uint64_t i = lo; i < hi; ++i) bounds = box_union(bounds, prims[i].box);
+        if (hi - lo <= 1) return ~(int32_t)(tri_base + lo);
+        const uint64_t mid = split(lo, hi, level);
+        const int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box3 lb, rb;
+        const int32_t l = build(lo, mid, level + 1, lb);
+        const int32_t r = build(mid, hi, level + 1, rb);
+        vr::Node& nd = nodes[me];
+        std::memset(&nd, 0, sizeof nd);
+        box_to_layout(lb, nd.box[0]);
+        box_to_layout(rb, nd.box[1]);
+        nd.child[0] = l;
+        nd.child[1] = r;
+        return me;
+    }
+};
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -510,6 +627,8 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     // device build: requested, a device exists for it, and no NaN coordinate (the reference's
     // sort comparator maps NaN to Equal, which only the host build reproduces)
     s->device_bvh = (flags & VR_SCENE_DEVICE_BVH) != 0 && !s->host_only;
+    // traversal tree: SAH (default) or the reference's own median-split tree
+    const bool sah = (flags & VR_SCENE_REFERENCE_BVH) == 0 && !s->device_bvh;
     for (uint32_t mi = 0; s->device_bvh && mi < desc->mesh_count; ++mi) {
         const vr_mesh_desc& m = desc->meshes[mi];
         if (m.triangle_count && !m.vertices) break;
@@ -558,6 +677,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
             continue;
         }
         BvhBuilder B;
+        std::vector<uint64_t> traversal_rank(m.triangle_count);
         B.tri_base = (int)s->tris.size();
         s->mesh_tri_base[mi] = B.tri_base;
         B.prims.resize(m.triangle_count);
@@ -585,6 +705,21 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
             B.nodes.reserve(m.triangle_count);
             int32_t root = B.build(0, m.triangle_count, 0, rb);
             box_to_layout(rb, bvh.root_box);
+            if (sah) {
+                // the traversal tree: SAH over the reference-ordered triangles (orig = rank)
+                std::vector<BuildPrim> sp(B.prims);
+                for (uint64_t i = 0; i < m.triangle_count; ++i) sp[i].orig = i;
+                SahBuilder T(sp);
+                T.tri_base = B.tri_base;
+                T.nodes.reserve(m.triangle_count);
+                Box3 trb;
+                root = T.build(0, m.triangle_count, 0, trb);
+                B.nodes.swap(T.nodes);
+                B.max_depth = T.max_depth;
+                for (uint64_t i = 0; i < m.triangle_count; ++i) traversal_rank[i] = sp[i].orig;
+            } else {
+                for (uint64_t i = 0; i < m.triangle_count; ++i) traversal_rank[i] = i;
+            }
             // re-base interior node indices into the scene-wide node array
             const int32_t node_base = (int32_t)s->nodes.size();
             for (auto& n : B.nodes)
@@ -595,13 +730,15 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
             s->max_depth = std::max(s->max_depth, B.max_depth);
         }
         s->leaf_order[mi].resize(m.triangle_count);
+        for (uint64_t i = 0; i < m.triangle_count; ++i) s->leaf_order[mi][i] = B.prims[i].orig;
         for (uint64_t i = 0; i < m.triangle_count; ++i) {
-            const uint64_t t = B.prims[i].orig;
-            s->leaf_order[mi][i] = t;
+            const uint64_t r = traversal_rank[i];  // reference leaf position of traversal leaf i
+            const uint64_t t = B.prims[r].orig;
             vr::TriVerts tv{};
             vr::TriNormals tn{};
             std::memcpy(tv.v, m.vertices + 9 * t, 9 * sizeof(double));
             std::memcpy(tn.n, m.normals + 9 * t, 9 * sizeof(double));
+            tv.rank = (int64_t)B.tri_base + (int64_t)r;
             s->tris.push_back(tv);
             s->normals.push_back(tn);
         }

@@ -36,10 +36,15 @@ struct alignas(64) Node32 {
 };
 static_assert(sizeof(Node32) == 64, "Node32 must be 64 B");
 
-// Triangle vertices in BVH leaf order, padded to 80 B for 16-B aligned loads.
+// Triangle vertices in traversal-BVH leaf order, 80 B for 16-B aligned loads.  `rank` is the
+// triangle's scene-wide position in the REFERENCE tree's in-order leaf sequence (tri_base + leaf
+// position of the median-split build): equal-distance hits go to the higher rank, as
+// closest_intersection's `b` wins ties (bounding_volume_hierarchy.rs:77-92).  The traversal
+// tree itself may differ from the reference's (the reference's result does
+// not depend on its topology).
 struct alignas(16) TriVerts {
     double v[9];
-    double pad;
+    int64_t rank;
 };
 static_assert(sizeof(TriVerts) == 80, "TriVerts must be 80 B");
 

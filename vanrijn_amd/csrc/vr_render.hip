@@ -149,7 +149,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         if (d < 0.0) return;
         bool take;
         if (!best.kind || d < best.d) take = true;
-        else if (d == best.d) take = (best.object == cur_object) ? (tri > best.index) : (cur_object < best.object);
+        else if (d == best.d)
+            take = (best.object == cur_object) ? (S.tris[tri].rank > S.tris[best.index].rank) : (cur_object < best.object);
         else take = false;
         if (take) {
             best.d = d;
@@ -622,7 +623,8 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
     out->primitive = best.kind == kPrim ? A.scene.prims[best.index].position : best.index;
     if (best.kind == kTri) {
         for (int b = 0; b < A.scene.bvh_count; ++b)
-            if (A.scene.bvhs[b].object == best.object) out->primitive = best.index - A.scene.bvhs[b].tri_base;
+            if (A.scene.bvhs[b].object == best.object)
+                out->primitive = A.scene.tris[best.index].rank - A.scene.bvhs[b].tri_base;  // reference leaf position
     }
     out->distance = best.d;
     out->location[0] = h.loc.x; out->location[1] = h.loc.y; out->location[2] = h.loc.z;

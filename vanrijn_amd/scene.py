@@ -248,18 +248,19 @@ class Scene:
             self._spec = SceneSpec(self.camera_location, mats, meshes, objs)
         return self._spec
 
-    def device_scene(self, device=0, host_only=False, device_bvh=False):
-        key = (device, host_only, device_bvh)
+    def device_scene(self, device=0, host_only=False, device_bvh=False, reference_bvh=False):
+        key = (device, host_only, device_bvh, reference_bvh)
         if key not in self._device_scenes:
-            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh)
+            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh, reference_bvh)
         return self._device_scenes[key]
 
 
 class DeviceScene:
     """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
 
-    def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False):
-        """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH; same nodes and leaf order)."""
+    def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False, reference_bvh=False):
+        """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH: the reference's tree);
+        reference_bvh: traverse the reference's median-split tree instead of the SAH tree."""
         L = N.lib()
         self.spec = spec
         keep = []  # keep ctypes buffers alive during vr_scene_create
@@ -291,7 +292,8 @@ class DeviceScene:
         desc = N.SceneDesc(N.Vec3(*spec.camera_location), len(spec.materials), len(prims), len(meshes), len(objs),
                            mats, prim_arr, mesh_arr, obj_arr)
         h = C.c_void_p()
-        flags = (N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0)
+        flags = ((N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0) |
+                 (N.SCENE_REFERENCE_BVH if reference_bvh else 0))
         N.check(L.vr_scene_create(C.byref(desc), device, flags, C.byref(h)))
         self.handle = h
         self.device = device
