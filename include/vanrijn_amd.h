@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 1
+#define VR_ABI_VERSION 2
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -58,15 +58,18 @@ typedef struct vr_spectrum {
 
 typedef enum vr_material_kind {
     VR_MATERIAL_LAMBERTIAN = 0, /* materials/lambertian_material.rs:12-60 */
-    VR_MATERIAL_REFLECTIVE = 1  /* materials/reflective_material.rs:8-48 */
+    VR_MATERIAL_REFLECTIVE = 1, /* materials/reflective_material.rs:8-48 */
+    VR_MATERIAL_PHONG = 2,      /* materials/phong_material.rs:8-37 (sample: materials/mod.rs:28-33) */
+    VR_MATERIAL_DIELECTRIC = 3  /* materials/smooth_transparent_dialectric.rs:64-115 (colour = eta) */
 } vr_material_kind;
 
 typedef struct vr_material_desc {
     int32_t kind;
     uint32_t reserved;
-    vr_spectrum colour;
-    double diffuse_strength;
-    double reflection_strength; /* reflective only */
+    vr_spectrum colour;         /* the refractive index eta(lambda) for the dielectric */
+    double diffuse_strength;    /* Lambertian, reflective, Phong */
+    double reflection_strength; /* reflective; Phong's specular_strength */
+    double smoothness;          /* Phong only */
 } vr_material_desc;
 
 typedef enum vr_primitive_kind {

@@ -17,6 +17,8 @@ MODE_REFERENCE = 0
 MODE_PRUNED = 1
 MATERIAL_LAMBERTIAN = 0
 MATERIAL_REFLECTIVE = 1
+MATERIAL_PHONG = 2
+MATERIAL_DIELECTRIC = 3
 PRIM_PLANE = 0
 PRIM_SPHERE = 1
 
@@ -79,7 +81,7 @@ def lib():
             "orc_merge_tile": (None, [u64, p, p, u64, u64, u64, u64, p, p]),
             "orc_scene_new": (p, [p]),
             "orc_scene_free": (None, [p]),
-            "orc_scene_add_material": (C.c_int, [p, i32, d, d, i32, p, d, d]),
+            "orc_scene_add_material": (C.c_int, [p, i32, d, d, i32, p, d, d, d]),
             "orc_scene_add_primitive_list": (C.c_int, [p, i32, p, p, p, p]),
             "orc_scene_add_mesh": (C.c_int, [p, i64, p, p, i32]),
             "orc_scene_mesh_leaf_order": (C.c_int, [p, i32, p]),
@@ -225,7 +227,7 @@ class OracleScene:
             s = f64(m.colour.samples)
             r = L.orc_scene_add_material(self.handle, m.kind, m.colour.shortest_wavelength,
                                          m.colour.longest_wavelength, s.size, _ptr(s), m.diffuse_strength,
-                                         m.reflection_strength)
+                                         m.reflection_strength, getattr(m, "smoothness", 0.0))
             assert r >= 0
         for obj in spec.objects:
             if obj.kind == "primitives":

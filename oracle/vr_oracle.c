@@ -59,6 +59,9 @@ typedef struct orc_rng {
 
 static double rng_standard(orc_rng* r) { return orc_u64_to_standard(orc_stream_draw(r->base, r->k++)); }
 static double rng_open01(orc_rng* r) { return orc_u64_to_open01(orc_stream_draw(r->base, r->k++)); }
+/* rand 0.7 Standard bool = (next_u32() as i32) < 0 with next_u32 = the draw's high half
+ * (smooth_transparent_dialectric.rs:103) */
+static int rng_bool(orc_rng* r) { return (int32_t)(uint32_t)(orc_stream_draw(r->base, r->k++) >> 32) < 0; }
 
 /* ======================================================================================== */
 /* Vec3 / Mat3 (src/math/vec3.rs, src/math/mat3.rs, src/math/mat2.rs)                     */
@@ -571,7 +574,8 @@ typedef struct orc_material {
     double shortest, longest;
     int n;
     double s[64];
-    double diffuse, reflection;
+    double diffuse, reflection; /* reflection = Phong's specular_strength */
+    double smoothness;          /* Phong */
 } orc_material;
 
 typedef struct orc_prim {
@@ -632,7 +636,7 @@ void orc_scene_free(orc_scene* s) {
     free(s);
 }
 int orc_scene_add_material(orc_scene* s, int32_t kind, double shortest, double longest, int32_t n,
-                           const double* samples, double diffuse, double reflection) {
+                           const double* samples, double diffuse, double reflection, double smoothness) {
     if (n < 1 || n > 64) return -1;
     s->mats = (orc_material*)realloc(s->mats, sizeof(orc_material) * (s->nmats + 1));
     orc_material* m = &s->mats[s->nmats];
@@ -644,6 +648,7 @@ int orc_scene_add_material(orc_scene* s, int32_t kind, double shortest, double l
     memcpy(m->s, samples, sizeof(double) * n);
     m->diffuse = diffuse;
     m->reflection = reflection;
+    m->smoothness = smoothness;
     return s->nmats++;
 }
 static void grow_objs(orc_scene* s) { s->objs = (orc_object*)realloc(s->objs, sizeof(orc_object) * (s->nobjs + 1)); }
@@ -940,11 +945,88 @@ static double mat_colour(const orc_material* m, double wl) {
     return orc_spectrum_intensity(m->shortest, m->longest, m->n, m->s, wl);
 }
 
-/* lambertian_material.rs:36-59 / reflective_material.rs:42-47 */
-static void material_sample(const orc_material* m, v3 w_i, orc_rng* rng, v3* w_o, double* pdf) {
+#define ORC_PI 3.14159265358979323846 /* std::f64::consts::PI */
+
+/* CosineWeightedHemisphere::value (random_distributions/cosine_weighted_hemisphere.rs:20-29)
+ * over UnitDisc::value (unit_disc.rs:28-40) over UniformSquare::value (uniform_square.rs:21-26):
+ * corner (-1, -1) + (Open01, Open01) * 2, x drawn first */
+static v3 cosine_weighted_hemisphere(orc_rng* rng) {
+    double ux = rng_open01(rng);
+    double uy = rng_open01(rng);
+    double ox = -1.0 + ux * 2.0, oy = -1.0 + uy * 2.0;
+    double px = ox, py = oy;
+    if (!(ox == 0.0 && oy == 0.0)) {
+        double radius, angle;
+        if (fabs(ox) > fabs(oy)) {
+            radius = ox;
+            angle = ((ORC_PI / 4.0) * oy) / ox;
+        } else {
+            radius = oy;
+            angle = ORC_PI / 2.0 - ((ORC_PI / 4.0) * ox) / oy;
+        }
+        px = cos(angle) * radius;
+        py = sin(angle) * radius;
+    }
+    return mk(px, py, sqrt(fmax(0.0, 1.0 - px * px - py * py)));
+}
+/* CosineWeightedHemisphere::pdf (cosine_weighted_hemisphere.rs:31-33) */
+static double cosine_weighted_pdf(v3 v) { return sqrt(v.x * v.x + v.y * v.y) / ORC_PI; }
+
+/* smooth_transparent_dialectric.rs:15-62 */
+typedef struct fresnel_result {
+    v3 rdir, tdir;
+    double R, T;
+} fresnel_result;
+static fresnel_result fresnel(v3 w_i, double eta1, double eta2) {
+    fresnel_result f;
+    v3 normal = w_i.z > 0.0 ? mk(0.0, 0.0, 1.0) : mk(-0.0, -0.0, -1.0); /* -Vec3::unit_z() */
+    f.rdir = mk(-w_i.x, -w_i.y, w_i.z);
+    double r = eta1 / eta2;
+    double c1 = dot(normal, w_i);
+    double c2sq = 1.0 - r * r * (1.0 - c1 * c1);
+    if (c2sq >= 0.0) {
+        double c2 = sqrt(c2sq);
+        double rpar = (eta1 * c2 - eta2 * c1) / (eta1 * c2 + eta2 * c1);
+        double rper = (eta1 * c1 - eta2 * c2) / (eta1 * c1 + eta2 * c2);
+        f.R = 0.5 * (rpar * rpar + rper * rper);
+        double k = r * c1 - c2;
+        f.tdir = normalize(mk(-r * w_i.x + k * normal.x, -r * w_i.y + k * normal.y, -r * w_i.z + k * normal.z));
+        f.T = 1.0 - f.R;
+    } else {
+        f.R = 1.0;
+        f.T = 0.0;
+        f.tdir = mk(0.0, 0.0, 0.0);
+    }
+    if (w_i.z < 0.0) {
+        f.rdir.z *= -1.0;
+        f.tdir.z *= -1.0;
+    }
+    return f;
+}
+static fresnel_result dielectric_fresnel(const orc_material* m, v3 w_i, double wl) {
+    double eta = orc_spectrum_intensity(m->shortest, m->longest, m->n, m->s, wl);
+    return w_i.z >= 0.0 ? fresnel(w_i, 1.0, eta) : fresnel(w_i, eta, 1.0);
+}
+
+/* lambertian_material.rs:36-59 / reflective_material.rs:42-47 / Material::sample's default for
+ * Phong (materials/mod.rs:28-33) / smooth_transparent_dialectric.rs:97-114 */
+static void material_sample(const orc_material* m, v3 w_i, double wl, orc_rng* rng, v3* w_o, double* pdf) {
     if (m->kind == ORC_MATERIAL_REFLECTIVE) {
         *w_o = mk(-w_i.x, -w_i.y, w_i.z);
         *pdf = 1.0;
+        return;
+    }
+    if (m->kind == ORC_MATERIAL_PHONG) {
+        *w_o = cosine_weighted_hemisphere(rng);
+        *pdf = cosine_weighted_pdf(*w_o);
+        return;
+    }
+    if (m->kind == ORC_MATERIAL_DIELECTRIC) {
+        fresnel_result f = dielectric_fresnel(m, w_i, wl);
+        *pdf = 0.5;
+        if (f.T <= 0.0000000001) *w_o = f.rdir;
+        else if (f.R <= 0.0000000001 || rng_bool(rng)) *w_o = f.tdir; /* random() only if needed */
+        else *w_o = f.rdir;
         return;
     }
     double x = 2.0 * rng_open01(rng) - 1.0;
@@ -983,6 +1065,26 @@ static photon material_bsdf(const orc_material* m, v3 w_o, v3 w_i, photon in) {
         out.intensity = out.intensity * (1.0 - f) + f;
         return out;
     }
+    if (m->kind == ORC_MATERIAL_PHONG) { /* phong_material.rs:17-36 */
+        out.wavelength = in.wavelength;
+        if (w_i.z < 0.0 || w_o.z < 0.0) {
+            out.intensity = 0.0;
+            return out;
+        }
+        v3 refl = mk(-w_i.x, -w_i.y, w_i.z);
+        out.intensity = (in.intensity * mat_colour(m, in.wavelength)) * m->diffuse +
+                        pow(fabs(dot(w_o, refl)), m->smoothness) * (m->reflection / dot(w_i, mk(0.0, 0.0, 1.0)));
+        return out;
+    }
+    if (m->kind == ORC_MATERIAL_DIELECTRIC) { /* smooth_transparent_dialectric.rs:79-95 */
+        fresnel_result f = dielectric_fresnel(m, w_i, in.wavelength);
+        v3 dr = sub(w_o, f.rdir), dt = sub(w_o, f.tdir);
+        out.wavelength = in.wavelength;
+        if (dot(dr, dr) < 0.0000000001) out.intensity = in.intensity * f.R;
+        else if (dot(dt, dt) < 0.0000000001) out.intensity = in.intensity * f.T;
+        else out.intensity = 0.0;
+        return out;
+    }
     out.wavelength = in.wavelength;
     out.intensity = in.intensity * mat_colour(m, in.wavelength);
     out.intensity *= m->diffuse;
@@ -1015,7 +1117,7 @@ static photon integrate(path_ctx* pc, const orc_hit* info, photon ph, int limit)
     const orc_material* m = &pc->s->mats[info->material];
     v3 w_o;
     double pdf;
-    material_sample(m, w_i, pc->rng, &w_o, &pdf);
+    material_sample(m, w_i, ph.wavelength, pc->rng, &w_o, &pdf);
     v3 wo_world = mul_mv(&bsdf_to_world, w_o);
     ray r0 = ray_new(ld(info->location), wo_world);
     ray r = ray_bias(&r0, 0.0000001);

@@ -83,13 +83,13 @@ void orc_merge_tile(uint64_t dst_width, double* dst_colour, double* dst_weight, 
 
 /* ---- scene ---- */
 typedef struct orc_scene orc_scene;
-enum { ORC_MATERIAL_LAMBERTIAN = 0, ORC_MATERIAL_REFLECTIVE = 1 };
+enum { ORC_MATERIAL_LAMBERTIAN = 0, ORC_MATERIAL_REFLECTIVE = 1, ORC_MATERIAL_PHONG = 2, ORC_MATERIAL_DIELECTRIC = 3 };
 enum { ORC_PRIM_PLANE = 0, ORC_PRIM_SPHERE = 1 };
 
 orc_scene* orc_scene_new(const double camera[3]);
 void orc_scene_free(orc_scene*);
-int orc_scene_add_material(orc_scene*, int32_t kind, double shortest, double longest, int32_t n,
-                           const double* samples, double diffuse, double reflection);
+int orc_scene_add_material(orc_scene*, int32_t kind, double shortest, double longest, int32_t n, const double* samples,
+                           double diffuse, double reflection, double smoothness);
 /* One object = Vec<Box<dyn Primitive>> (vec_aggregate.rs:11-22): kinds/materials/vecs(3 each)/scalars */
 int orc_scene_add_primitive_list(orc_scene*, int32_t count, const int32_t* kinds, const int32_t* materials,
                                  const double* vecs, const double* scalars);

@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_struct_sizes_match_header():
     assert C.sizeof(N.Spectrum) == 32
-    assert C.sizeof(N.MaterialDesc) == 56
+    assert C.sizeof(N.MaterialDesc) == 64
     assert C.sizeof(N.PrimitiveDesc) == 40
     assert C.sizeof(N.MeshDesc) == 32
     assert C.sizeof(N.ObjectDesc) == 16
@@ -40,7 +40,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 1
+    assert lib.vr_abi_version() == 2
     assert isinstance(lib.vr_last_error(), bytes)
 
 

@@ -15,7 +15,7 @@ STATUS = {
     -4: "VR_ERROR_NO_DEVICE", -5: "VR_ERROR_SINGULAR_BASIS", -6: "VR_ERROR_IO", -7: "VR_ERROR_UNSUPPORTED",
     -8: "VR_ERROR_HOST_ONLY",
 }
-MATERIAL_LAMBERTIAN, MATERIAL_REFLECTIVE = 0, 1
+MATERIAL_LAMBERTIAN, MATERIAL_REFLECTIVE, MATERIAL_PHONG, MATERIAL_DIELECTRIC = 0, 1, 2, 3
 PRIMITIVE_PLANE, PRIMITIVE_SPHERE = 0, 1
 OBJECT_PRIMITIVE_LIST, OBJECT_BVH = 0, 1
 SCENE_HOST_ONLY = 1
@@ -41,7 +41,7 @@ class Spectrum(C.Structure):
 
 class MaterialDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("reserved", C.c_uint32), ("colour", Spectrum),
-                ("diffuse_strength", C.c_double), ("reflection_strength", C.c_double)]
+                ("diffuse_strength", C.c_double), ("reflection_strength", C.c_double), ("smoothness", C.c_double)]
 
 
 class PrimitiveDesc(C.Structure):

@@ -70,6 +70,9 @@ struct Rng {
     __device__ __forceinline__ double open01() {
         return __longlong_as_double((long long)((next() >> 12) | 0x3FF0000000000000ull)) - (1.0 - 0x1.0p-53);
     }
+    // rand 0.7 Standard bool, `(next_u32() as i32) < 0` (smooth_transparent_dialectric.rs:103):
+    // the u32 is the draw's high half, so the bool is the draw's top bit
+    __device__ __forceinline__ bool boolean() { return (int32_t)(uint32_t)(next() >> 32) < 0; }
 };
 __device__ __forceinline__ uint64_t stream_base(uint64_t seed, uint64_t pixel, uint64_t sample) {
     uint64_t k = mix64(seed ^ kSeedSalt);
@@ -98,6 +101,81 @@ __device__ __forceinline__ double spectrum_at(double shortest, double longest, i
 
 __device__ __forceinline__ double material_colour(const Material* m, double wl) {
     return spectrum_at(m->shortest, m->longest, m->n, wl, [&](int j) { return m->samples[j]; });
+}
+
+// ----------------------------------------------------------------------------------------------
+// Phong and dielectric materials (materials/phong_material.rs, smooth_transparent_dialectric.rs)
+// ----------------------------------------------------------------------------------------------
+constexpr double kPi = 3.14159265358979323846;  // std::f64::consts::PI
+
+// Material::sample's default, CosineWeightedHemisphere::value (cosine_weighted_hemisphere.rs:20-
+// 29) over UnitDisc (unit_disc.rs:28-40, Shirley's concentric map) over UniformSquare
+// (uniform_square.rs:21-26: corner + (Open01, Open01) * size, x drawn first)
+__device__ __forceinline__ V3 cosine_weighted_hemisphere(Rng& rng) {
+    const double ux = rng.open01();
+    const double uy = rng.open01();
+    const double ox = -1.0 + ux * 2.0, oy = -1.0 + uy * 2.0;
+    double px = ox, py = oy;
+    if (!(ox == 0.0 && oy == 0.0)) {
+        double radius, angle;
+        if (fabs(ox) > fabs(oy)) {
+            radius = ox;
+            angle = ((kPi / 4.0) * oy) / ox;
+        } else {
+            radius = oy;
+            angle = kPi / 2.0 - ((kPi / 4.0) * ox) / oy;
+        }
+        px = cos(angle) * radius;
+        py = sin(angle) * radius;
+    }
+    const double z = sqrt(fmax(0.0, 1.0 - px * px - py * py));
+    return mk(px, py, z);
+}
+__device__ __forceinline__ double cosine_weighted_pdf(V3 v) { return sqrt(v.x * v.x + v.y * v.y) / kPi; }
+
+// fresnel (smooth_transparent_dialectric.rs:15-62)
+struct Fresnel {
+    V3 rdir, tdir;
+    double R, T;
+};
+__device__ __forceinline__ Fresnel fresnel(V3 w_i, double eta1, double eta2) {
+    Fresnel f;
+    const V3 normal = w_i.z > 0.0 ? mk(0.0, 0.0, 1.0) : mk(-0.0, -0.0, -1.0);  // -Vec3::unit_z()
+    f.rdir = mk(-w_i.x, -w_i.y, w_i.z);
+    const double r = eta1 / eta2;
+    const double c1 = dot(normal, w_i);
+    const double c2sq = 1.0 - r * r * (1.0 - c1 * c1);
+    if (c2sq >= 0.0) {
+        const double c2 = sqrt(c2sq);
+        const double rpar = (eta1 * c2 - eta2 * c1) / (eta1 * c2 + eta2 * c1);
+        const double rper = (eta1 * c1 - eta2 * c2) / (eta1 * c1 + eta2 * c2);
+        f.R = 0.5 * (rpar * rpar + rper * rper);
+        const double k = r * c1 - c2;
+        f.tdir = normalize(add(mk(-r * w_i.x, -r * w_i.y, -r * w_i.z), mk(k * normal.x, k * normal.y, k * normal.z)));
+        f.T = 1.0 - f.R;
+    } else {
+        f.R = 1.0;
+        f.T = 0.0;
+        f.tdir = mk(0.0, 0.0, 0.0);
+    }
+    if (w_i.z < 0.0) {
+        f.rdir.z *= -1.0;
+        f.tdir.z *= -1.0;
+    }
+    return f;
+}
+// eta pair by side (smooth_transparent_dialectric.rs:81-86,94-99)
+__device__ __forceinline__ Fresnel dielectric_fresnel(const Material* m, V3 w_i, double wl) {
+    const double eta = material_colour(m, wl);
+    return w_i.z >= 0.0 ? fresnel(w_i, 1.0, eta) : fresnel(w_i, eta, 1.0);
+}
+// the bsdf's strength for an outgoing direction (smooth_transparent_dialectric.rs:88-95)
+__device__ __forceinline__ double dielectric_strength(const Fresnel& f, V3 w_o) {
+    const V3 dr = sub(w_o, f.rdir);
+    if (dot(dr, dr) < 0.0000000001) return f.R;
+    const V3 dt = sub(w_o, f.tdir);
+    if (dot(dt, dt) < 0.0000000001) return f.T;
+    return 0.0;
 }
 
 // test_lighting_environment (simple_random_integrator.rs:57-65): reflection_from_linear_rgb of

@@ -561,7 +561,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
 
     for (uint32_t i = 0; i < desc->material_count; ++i) {
         const vr_material_desc& m = desc->materials[i];
-        if (m.kind != VR_MATERIAL_LAMBERTIAN && m.kind != VR_MATERIAL_REFLECTIVE) return bad("unknown material kind");
+        if (m.kind < VR_MATERIAL_LAMBERTIAN || m.kind > VR_MATERIAL_DIELECTRIC) return bad("unknown material kind");
         if (m.colour.sample_count < 1 || m.colour.sample_count > VR_MAX_SPECTRUM_SAMPLES || !m.colour.samples)
             return bad("material spectrum needs 1..64 samples");
         vr::Material dm{};
@@ -571,10 +571,14 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         dm.longest = m.colour.longest_wavelength;
         dm.diffuse = m.diffuse_strength;
         dm.reflection = m.reflection_strength;
+        dm.smoothness = m.smoothness;
         std::memcpy(dm.samples, m.colour.samples, sizeof(double) * m.colour.sample_count);
         s->materials.push_back(dm);
         if (vr_spectrum_intensity_at_wavelength(&m.colour, 0.0) != 0.0) s->dark0 = false;
-        s->mats |= m.kind == VR_MATERIAL_REFLECTIVE ? 2 : 1;
+        s->mats |= m.kind == VR_MATERIAL_LAMBERTIAN ? 1 : (m.kind == VR_MATERIAL_REFLECTIVE ? 2 : 4);
+        // the dielectric's strength at 0 nm is not its eta(0): a path cut at the recursion limit
+        // (lambda 0) needs the general lambda-0 chain
+        if (m.kind == VR_MATERIAL_DIELECTRIC) s->dark0 = false;
     }
     // objects: primitive lists keep their order; BVHs are built per mesh
     std::vector<int> mesh_object(desc->mesh_count, -1);

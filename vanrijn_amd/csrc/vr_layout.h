@@ -55,11 +55,11 @@ struct alignas(16) TriNormals {
 };
 
 struct Material {
-    int32_t kind;  // 0 Lambertian, 1 Reflective
-    int32_t n;     // spectrum sample count
+    int32_t kind;  // 0 Lambertian, 1 Reflective, 2 Phong, 3 smooth transparent dielectric
+    int32_t n;     // spectrum sample count (colour; the refractive index for the dielectric)
     double shortest, longest;
-    double diffuse, reflection;
-    double pad;
+    double diffuse, reflection;  // reflection = Phong's specular_strength
+    double smoothness;           // Phong exponent
     double samples[kMaxSpectrumSamples];
 };
 

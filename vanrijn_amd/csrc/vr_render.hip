@@ -259,10 +259,22 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         const Material* mat = &S.materials[h.material];
         V3 w_o;
         double pdf;
-        const bool reflective = MATS == 2 || (MATS == 3 && mat->kind == 1);
-        if (reflective) {  // reflective_material.rs:42-47
+        // material kind: compiled in for the kinds the scene has (MATS 1: Lambertian only,
+        // 2: reflective only, 3: any of Lambertian / reflective / Phong / dielectric)
+        const int kind = MATS == 1 ? 0 : (MATS == 2 ? 1 : mat->kind);
+        Fresnel fr;  // dielectric only
+        if (kind == 1) {  // reflective_material.rs:42-47
             w_o = mk(-w_i.x, -w_i.y, w_i.z);
             pdf = 1.0;
+        } else if (MATS == 3 && kind == 2) {  // Phong: Material::sample's default (materials/mod.rs:28-33)
+            w_o = cosine_weighted_hemisphere(rng);
+            pdf = cosine_weighted_pdf(w_o);
+        } else if (MATS == 3 && kind == 3) {  // smooth_transparent_dialectric.rs:97-114
+            fr = dielectric_fresnel(mat, w_i, lambda);
+            pdf = 0.5;
+            if (fr.T <= 0.0000000001) w_o = fr.rdir;
+            else if (fr.R <= 0.0000000001 || rng.boolean()) w_o = fr.tdir;
+            else w_o = fr.rdir;
         } else {  // lambertian_material.rs:36-59: rejection sampling on Open01 pairs
             double x = 2.0 * rng.open01() - 1.0;
             double y = 2.0 * rng.open01() - 1.0;
@@ -297,7 +309,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         const double c_l = material_colour(mat, lambda);
         const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
         double a, a0, bterm;
-        if (reflective) {  // reflective_material.rs:17-39
+        if (kind == 1) {  // reflective_material.rs:17-39
             if (w_i.z <= 0.0 || w_o.z <= 0.0) {
                 a = 0.0; a0 = 0.0; bterm = 0.0;
             } else {
@@ -311,6 +323,19 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 a0 = (((pdf * cosf) * c_0) * mat->diffuse) * (1.0 - f);
                 bterm = f;
             }
+        } else if (MATS == 3 && kind == 2) {  // phong_material.rs:17-36: diffuse + specular lobe
+            if (w_i.z < 0.0 || w_o.z < 0.0) {
+                a = 0.0; a0 = 0.0; bterm = 0.0;
+            } else {
+                const V3 refl = mk(-w_i.x, -w_i.y, w_i.z);
+                a = ((pdf * cosf) * c_l) * mat->diffuse;
+                a0 = ((pdf * cosf) * c_0) * mat->diffuse;
+                bterm = pow(fabs(dot(w_o, refl)), mat->smoothness) * (mat->reflection / dot(w_i, mk(0.0, 0.0, 1.0)));
+            }
+        } else if (MATS == 3 && kind == 3) {  // smooth_transparent_dialectric.rs:79-95
+            a = (pdf * cosf) * dielectric_strength(fr, w_o);
+            a0 = DARK0 ? 0.0 : (pdf * cosf) * dielectric_strength(dielectric_fresnel(mat, w_i, 0.0), w_o);
+            bterm = 0.0;
         } else {  // lambertian_material.rs:27-34
             a = ((pdf * cosf) * c_l) * mat->diffuse;
             a0 = ((pdf * cosf) * c_0) * mat->diffuse;
@@ -464,15 +489,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 bool h0 = r0 == 1 && !(f0 > cull_far || g0 < cull_behind);
                 bool h1 = r1 == 1 && !(f1 > cull_far || g1 < cull_behind);
                 if (r0 == 2 || r1 == 2) { VR_SEC(2); }
-                if (r0 == 2) {  // too close to call in f32: the exact test and the f64 cull
+                // too close to call in f32: the exact test and the f64 cull, one inlined copy
+                // run once per undecided child
+                bool x0 = r0 == 2, x1 = r1 == 2;
+                while (x0 || x1) {
+                    const int c = x0 ? 0 : 1;
                     if (COUNT) cnt.exact_boxes++;
                     double lo, hi;
-                    h0 = slab(S.nodes[node].box[0], pre, lo, hi) && !culled(lo, hi);
-                }
-                if (r1 == 2) {
-                    if (COUNT) cnt.exact_boxes++;
-                    double lo, hi;
-                    h1 = slab(S.nodes[node].box[1], pre, lo, hi) && !culled(lo, hi);
+                    const bool h = slab(S.nodes[node].box[c], pre, lo, hi) && !culled(lo, hi);
+                    if (c == 0) { h0 = h; x0 = false; } else { h1 = h; x1 = false; }
                 }
                 // leaf: queue its triangle (selects, not stores through a pointer to the slot:
                 // that would demote p0..p3 to scratch memory)
@@ -649,6 +674,9 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
+    // kinds present (bit 0 Lambertian, 1 reflective, 2 Phong or dielectric) -> specialisation:
+    // Lambertian-only (1), reflective-only (2) or the general kernel (3)
+    mats = (mats == 1 || mats == 2) ? mats : 3;
     if (!dark0) mats = 3;  // the general kernel
     if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);  // experiment hook
 #define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)

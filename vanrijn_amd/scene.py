@@ -105,6 +105,26 @@ class ReflectiveMaterial:
     reflection_strength: float
 
 
+@dataclass
+class PhongMaterial:
+    """materials/phong_material.rs:8-37; sampled by CosineWeightedHemisphere (materials/mod.rs:28-33)."""
+    colour: Spectrum
+    diffuse_strength: float
+    specular_strength: float
+    smoothness: float
+
+
+@dataclass
+class SmoothTransparentDialectric:
+    """materials/smooth_transparent_dialectric.rs:64-115 (the reference's spelling): refractive index
+    eta(lambda) as a Spectrum."""
+    eta: Spectrum
+
+    @staticmethod
+    def new(eta):
+        return SmoothTransparentDialectric(eta)
+
+
 # ------------------------------------------------------------------------------ geometry
 @dataclass
 class Plane:
@@ -165,7 +185,8 @@ class MaterialSpec:
     kind: int
     colour: Spectrum
     diffuse_strength: float
-    reflection_strength: float = 0.0
+    reflection_strength: float = 0.0  # reflective; Phong's specular strength
+    smoothness: float = 0.0           # Phong
 
 
 @dataclass
@@ -222,6 +243,11 @@ class Scene:
                                                  m.reflection_strength))
                     elif isinstance(m, LambertianMaterial):
                         mats.append(MaterialSpec(N.MATERIAL_LAMBERTIAN, m.colour, m.diffuse_strength, 0.0))
+                    elif isinstance(m, PhongMaterial):
+                        mats.append(MaterialSpec(N.MATERIAL_PHONG, m.colour, m.diffuse_strength, m.specular_strength,
+                                                 m.smoothness))
+                    elif isinstance(m, SmoothTransparentDialectric):
+                        mats.append(MaterialSpec(N.MATERIAL_DIELECTRIC, m.eta, 0.0, 0.0))
                     else:
                         raise TypeError(f"unsupported material {type(m).__name__}")
                 return mat_ids[id(m)]
@@ -270,7 +296,7 @@ class DeviceScene:
             keep.append(s)
             mats[i] = N.MaterialDesc(m.kind, 0, N.Spectrum(m.colour.shortest_wavelength, m.colour.longest_wavelength,
                                                            s.size, s.ctypes.data_as(C.POINTER(C.c_double))),
-                                     m.diffuse_strength, m.reflection_strength)
+                                     m.diffuse_strength, m.reflection_strength, m.smoothness)
         prims, objs, meshes = [], [], []
         for o in spec.objects:
             if o.kind == "primitives":

@@ -20,8 +20,8 @@ import os
 
 import numpy as np
 
-from .scene import (BoundingVolumeHierarchy, ColourRgbF, LambertianMaterial, Mesh, NamedColour, Plane,
-                    ReflectiveMaterial, Scene, Sphere, Spectrum, load_obj)
+from .scene import (BoundingVolumeHierarchy, ColourRgbF, LambertianMaterial, Mesh, NamedColour, PhongMaterial, Plane,
+                    ReflectiveMaterial, Scene, SmoothTransparentDialectric, Spectrum, Sphere, load_obj)
 
 CAMERA_LOCATION = (-2.0, 1.0, -5.0)  # main.rs:139, simple_scene.rs:25
 BUNNY_SHA256 = "7ee71a949c270c53226056a0ad120e8a8dcdba54d36c2420f987dd1cdd4e302f"
@@ -187,6 +187,27 @@ def bench_scene(mesh=None):
     mat = ReflectiveMaterial(Spectrum.reflection_from_linear_rgb(ColourRgbF.from_named(NamedColour.Yellow)), 0.05,
                              0.9)
     return Scene(CAMERA_LOCATION, [BoundingVolumeHierarchy.build(Mesh(v, nrm, mat))])
+
+
+def materials_scene(mesh=None):
+    """main.rs's layout with every material kind: a Phong sphere, a glass sphere
+    (SmoothTransparentDialectric, eta 1.5), a reflective sphere, Lambertian plane and bunny.
+    The reference instantiates Phong and the dielectric nowhere; this scene exercises them."""
+    v, nrm = _mesh_arrays(mesh)
+    bunny = Mesh(v, nrm, LambertianMaterial(Spectrum.reflection_from_linear_rgb(ColourRgbF.from_named(
+        NamedColour.Yellow)), 0.05))
+    return Scene(CAMERA_LOCATION, [
+        [
+            Plane((0.0, 1.0, 0.0), -2.0, LambertianMaterial(
+                Spectrum.reflection_from_linear_rgb(ColourRgbF.new(0.55, 0.27, 0.04)), 0.1)),
+            Sphere((-6.25, -0.5, 1.0), 1.0, PhongMaterial(
+                Spectrum.reflection_from_linear_rgb(ColourRgbF.from_named(NamedColour.Green)), 0.1, 0.3, 40.0)),
+            Sphere((-4.25, -0.5, 2.0), 1.0, SmoothTransparentDialectric(Spectrum.grey(1.5))),
+            Sphere((-5.0, 1.5, 1.0), 1.0, ReflectiveMaterial(
+                Spectrum.reflection_from_linear_rgb(ColourRgbF.from_named(NamedColour.Red)), 0.05, 0.9)),
+        ],
+        BoundingVolumeHierarchy.build(bunny),
+    ])
 
 
 def synthetic_scene():
