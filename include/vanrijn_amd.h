@@ -108,6 +108,27 @@ typedef struct vr_object_desc {
 
 /* scene::Scene (src/scene.rs:5-8): camera_location + objects in order (order decides ties,
  * sampler.rs:9-20). */
+/* Integrators.  The reference's partial_render_scene always uses SimpleRandomIntegrator
+ * (camera.rs:103); WhittedIntegrator (integrators/whitted_integrator.rs:15-87: directional lights
+ * with shadow rays, an ambient term, one sampled continuation per hit) is selectable per scene. */
+typedef enum vr_integrator_kind {
+    VR_INTEGRATOR_SIMPLE_RANDOM = 0,
+    VR_INTEGRATOR_WHITTED = 1
+} vr_integrator_kind;
+
+typedef struct vr_directional_light { /* whitted_integrator.rs:10-13 */
+    vr_vec3 direction;
+    vr_spectrum spectrum;
+} vr_directional_light;
+
+typedef struct vr_integrator_desc {
+    int32_t kind;
+    uint32_t light_count;        /* at most VR_MAX_LIGHTS */
+    vr_spectrum ambient_light;   /* Whitted */
+    const vr_directional_light* lights;
+} vr_integrator_desc;
+#define VR_MAX_LIGHTS 16
+
 typedef struct vr_scene_desc {
     vr_vec3 camera_location;
     uint32_t material_count;
@@ -118,6 +139,7 @@ typedef struct vr_scene_desc {
     const vr_primitive_desc* primitives;
     const vr_mesh_desc* meshes;
     const vr_object_desc* objects;
+    const vr_integrator_desc* integrator; /* NULL: SimpleRandomIntegrator */
 } vr_scene_desc;
 
 typedef struct vr_scene vr_scene;

@@ -76,6 +76,7 @@ def lib():
             "orc_colour_xyz_from_linear_rgb": (None, [p, p]),
             "orc_sky_intensity": (d, [p, d]),
             "orc_tone_map": (None, [p, u64, p]),
+            "orc_scene_set_whitted": (C.c_int, [p, d, d, i32, p, i32, p, p, p, p, p]),
             "orc_ray_for_pixel": (None, [p, u64, u64, u64, u64, d, d, p, p]),
             "orc_update_pixel": (None, [p, p, p, p, p, d, d, d]),
             "orc_merge_tile": (None, [u64, p, p, u64, u64, u64, u64, p, p]),
@@ -229,6 +230,20 @@ class OracleScene:
                                          m.colour.longest_wavelength, s.size, _ptr(s), m.diffuse_strength,
                                          m.reflection_strength, getattr(m, "smoothness", 0.0))
             assert r >= 0
+        ig = getattr(spec, "integrator", None)
+        if ig is not None:  # WhittedIntegrator
+            amb = f64(ig.ambient_light.samples)
+            n = len(ig.lights)
+            dirs = f64([li.direction for li in ig.lights] or [[0.0, 0.0, 0.0]]).reshape(-1)
+            sh = f64([li.spectrum.shortest_wavelength for li in ig.lights] or [0.0])
+            lo = f64([li.spectrum.longest_wavelength for li in ig.lights] or [0.0])
+            cnt = np.array([len(li.spectrum.samples) for li in ig.lights] or [1], dtype=np.int32)
+            samp = np.zeros((max(n, 1), 64))
+            for j, li in enumerate(ig.lights):
+                samp[j, :len(li.spectrum.samples)] = li.spectrum.samples
+            assert L.orc_scene_set_whitted(self.handle, ig.ambient_light.shortest_wavelength,
+                                           ig.ambient_light.longest_wavelength, amb.size, _ptr(amb), n, _ptr(dirs),
+                                           _ptr(sh), _ptr(lo), cnt.ctypes.data_as(C.c_void_p), _ptr(samp)) == 0
         for obj in spec.objects:
             if obj.kind == "primitives":
                 kinds = np.array([p.kind for p in obj.primitives], dtype=np.int32)

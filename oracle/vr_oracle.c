@@ -607,6 +607,12 @@ typedef struct orc_object {
 
 struct orc_scene {
     v3 camera;
+    /* WhittedIntegrator (whitted_integrator.rs:15-87) when whitted != 0 */
+    int whitted;
+    orc_material ambient;
+    int nlights;
+    v3 light_dir[16];
+    orc_material light[16];
     orc_material* mats;
     int nmats;
     orc_prim* prims;
@@ -1138,6 +1144,87 @@ static photon integrate(path_ctx* pc, const orc_hit* info, photon ph, int limit)
     return material_bsdf(m, w_o, w_i, below);
 }
 
+/* whitted_integrator.rs:20-87.  The continuation ray at recursion limit 0 is not traced: the
+ * reference traces it and then discards it (`if recursion_limit > 0 ... else scale 0`), which
+ * changes no value; the bounce count records only traced continuations. */
+static photon whitted(path_ctx* pc, const orc_hit* info, photon ph, int limit) {
+    const orc_scene* s = pc->s;
+    photon zero = {ph.wavelength, 0.0};
+    m3 w2b = from_rows(ld(info->tangent), ld(info->cotangent), ld(info->normal));
+    m3 b2w;
+    if (!try_inverse(&w2b, &b2w)) { /* "Expected matrix to be invertable." */
+        pc->error = 1;
+        return zero;
+    }
+    const orc_material* m = &s->mats[info->material];
+    v3 w_ret = mul_mv(&w2b, ld(info->retro));
+    /* material.sample is evaluated when the iterator chain is built, before any light term */
+    v3 dir;
+    double pdf;
+    material_sample(m, w_ret, ph.wavelength, pc->rng, &dir, &pdf);
+    double acc = ph.intensity; /* fold(photon.clone(), ...) */
+    for (int j = 0; j < s->nlights; ++j) {
+        ray r0 = ray_new(ld(info->location), s->light_dir[j]);
+        ray r = ray_bias(&r0, 0.0000001);
+        orc_hit sh;
+        sample_scene(s, &r, pc->cx, &sh);
+        double term;
+        if (sh.valid) {
+            term = orc_spectrum_intensity(s->ambient.shortest, s->ambient.longest, s->ambient.n, s->ambient.s,
+                                          ph.wavelength); /* ambient_light.emit_photon */
+        } else {
+            const orc_material* L = &s->light[j];
+            photon in = {ph.wavelength, orc_spectrum_intensity(L->shortest, L->longest, L->n, L->s, ph.wavelength)};
+            in.intensity = in.intensity * fabs(dot(s->light_dir[j], ld(info->normal)));
+            term = material_bsdf(m, w_ret, mul_mv(&w2b, s->light_dir[j]), in).intensity;
+        }
+        acc = acc + term;
+    }
+    if (limit > 0) {
+        v3 wd = mul_mv(&b2w, dir);
+        ray c0 = ray_new(ld(info->location), wd);
+        ray c = ray_bias(&c0, 0.0000001);
+        pc->bounces++;
+        orc_hit next;
+        sample_scene(s, &c, pc->cx, &next);
+        if (next.valid) {
+            photon below = whitted(pc, &next, ph, limit - 1);
+            photon out = material_bsdf(m, w_ret, dir, below);
+            acc = acc + out.intensity * fabs(dot(wd, ld(info->normal)));
+        } else {
+            acc = acc + ph.intensity * 0.0;
+        }
+    } else {
+        pc->limit_hit = 1;
+        acc = acc + ph.intensity * 0.0;
+    }
+    photon out = {ph.wavelength, acc};
+    return out;
+}
+
+int orc_scene_set_whitted(orc_scene* s, double amb_shortest, double amb_longest, int32_t amb_n,
+                          const double* amb_samples, int32_t nlights, const double* dirs, const double* shortest,
+                          const double* longest, const int32_t* n, const double* samples) {
+    if (nlights < 0 || nlights > 16 || amb_n < 1 || amb_n > 64) return -1;
+    s->whitted = 1;
+    memset(&s->ambient, 0, sizeof s->ambient);
+    s->ambient.shortest = amb_shortest;
+    s->ambient.longest = amb_longest;
+    s->ambient.n = amb_n;
+    memcpy(s->ambient.s, amb_samples, sizeof(double) * amb_n);
+    s->nlights = nlights;
+    for (int j = 0; j < nlights; ++j) {
+        if (n[j] < 1 || n[j] > 64) return -1;
+        s->light_dir[j] = ld(dirs + 3 * j);
+        memset(&s->light[j], 0, sizeof s->light[j]);
+        s->light[j].shortest = shortest[j];
+        s->light[j].longest = longest[j];
+        s->light[j].n = n[j];
+        memcpy(s->light[j].s, samples + 64 * j, sizeof(double) * n[j]);
+    }
+    return 0;
+}
+
 /* One sample of one pixel: the body of camera.rs:105-127 */
 static void render_one(const orc_scene* s, trace_ctx* cx, uint64_t height, uint64_t width, uint64_t row, uint64_t col,
                        uint64_t seed, uint64_t sample, orc_sample_record* rec) {
@@ -1156,7 +1243,7 @@ static void render_one(const orc_scene* s, trace_ctx* cx, uint64_t height, uint6
         rec->flags |= 1;
         photon start = {SHORTEST_VISIBLE + (LONGEST_VISIBLE - SHORTEST_VISIBLE) * rng_standard(&rng), 0.0};
         path_ctx pc = {s, cx, &rng, 0, 0, 0};
-        ph = integrate(&pc, &hit, start, 128);
+        ph = s->whitted ? whitted(&pc, &hit, start, 128) : integrate(&pc, &hit, start, 128);
         rec->bounces = pc.bounces;
         if (pc.limit_hit) rec->flags |= 2;
         if (pc.error) { rec->flags |= 4; cx->cnt->errors++; }

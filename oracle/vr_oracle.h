@@ -136,6 +136,12 @@ int orc_render_samples(const orc_scene*, uint64_t start_column, uint64_t end_col
                        uint64_t end_row, uint64_t height, uint64_t width, uint32_t spp, uint64_t seed,
                        uint64_t first_sample, int32_t mode, int32_t nthreads, orc_sample_record* out);
 
+/* Render with WhittedIntegrator (whitted_integrator.rs:15-87) instead of SimpleRandomIntegrator:
+ * ambient spectrum + nlights (<= 16) directional lights (dirs [n][3]; spectra: samples [n][64]). */
+int orc_scene_set_whitted(orc_scene*, double amb_shortest, double amb_longest, int32_t amb_n,
+                          const double* amb_samples, int32_t nlights, const double* dirs, const double* shortest,
+                          const double* longest, const int32_t* n, const double* samples);
+
 /* AccumulationBuffer::to_image_rgb_u8(&ClampingToneMapper) on the colour buffer [n][3]. */
 void orc_tone_map(const double* colour, uint64_t n, uint8_t* rgb);
 

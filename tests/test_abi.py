@@ -32,7 +32,7 @@ def test_struct_sizes_match_header():
     assert C.sizeof(N.PrimitiveDesc) == 40
     assert C.sizeof(N.MeshDesc) == 32
     assert C.sizeof(N.ObjectDesc) == 16
-    assert C.sizeof(N.SceneDesc) == 72
+    assert C.sizeof(N.SceneDesc) == 80
     assert C.sizeof(N.RenderParams) == 72
     assert C.sizeof(N.SampleRecord) == 48
     assert C.sizeof(N.HitRecord) == 144

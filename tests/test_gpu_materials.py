@@ -47,3 +47,33 @@ def test_materials_image_l2(pair, oracle):
     err = np.sqrt(((got.colour_buffer - want["colour"]) ** 2).sum(axis=-1)).max()
     assert err < 1e-5
     assert np.array_equal(got.weight_buffer, want["weight"])
+
+
+@pytest.fixture(scope="module")
+def whitted_pair(oracle):
+    s = scenes.whitted_scene(scenes.procedural_bunny())
+    return s, oracle.OracleScene(s.spec())
+
+
+def test_whitted_samples_match_oracle(whitted_pair, oracle):
+    """integrators/whitted_integrator.rs:20-87: shadow rays per light, ambient term, one sampled
+    continuation per hit (its ray is not traced at recursion limit 0, where the reference
+    discards it)."""
+    s, orc = whitted_pair
+    tile = Tile(0, 64, 0, 48)
+    got = render_samples(s, tile, 48, 64, 3, SEED)
+    want = orc.render_samples(tile, 48, 64, 3, SEED, 0, oracle.MODE_REFERENCE, 8)
+    assert np.array_equal(got["flags"], want["flags"])
+    assert np.array_equal(got["bounces"], want["bounces"])
+    assert np.array_equal(got["wavelength"], want["wavelength"])
+    np.testing.assert_allclose(got["intensity"], want["intensity"], rtol=1e-12, atol=1e-300)
+    assert (got["intensity"] > 0).mean() > 0.2  # lights reach most hits
+
+
+def test_whitted_image_l2(whitted_pair, oracle):
+    s, orc = whitted_pair
+    t = Tile(0, 96, 0, 64)
+    got = render_tile(s, t, 64, 96, 4, SEED)
+    want = orc.render_tile(t, 64, 96, 4, SEED, 0, oracle.MODE_REFERENCE, 8)
+    err = np.sqrt(((got.colour_buffer - want["colour"]) ** 2).sum(axis=-1)).max()
+    assert err < 1e-5

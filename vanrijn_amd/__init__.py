@@ -6,8 +6,8 @@ library; every pixel is computed on the GPU.
 """
 from .render import (AccumulationBuffer, ImageRgbU8, Tile, TileIterator, partial_render_scene, render_samples,
                      render_tile, render_tile_device, resolve_state, tone_map_device, trace_rays)
-from .scene import (BoundingVolumeHierarchy, ColourRgbF, DeviceScene, LambertianMaterial, Mesh, NamedColour,
-                    PhongMaterial, Plane, ReflectiveMaterial, Scene, SceneSpec, SmoothTransparentDialectric, Sphere,
+from .scene import (BoundingVolumeHierarchy, ColourRgbF, DeviceScene, DirectionalLight, LambertianMaterial, Mesh,
+                    NamedColour, PhongMaterial, Plane, WhittedIntegrator, ReflectiveMaterial, Scene, SceneSpec, SmoothTransparentDialectric, Sphere,
                     Spectrum, load_obj)
 from . import _native
 
@@ -15,7 +15,7 @@ __all__ = [
     "AccumulationBuffer", "ImageRgbU8", "Tile", "TileIterator", "partial_render_scene", "render_samples", "render_tile",
     "render_tile_device", "resolve_state", "tone_map_device", "trace_rays", "BoundingVolumeHierarchy", "ColourRgbF", "DeviceScene",
     "LambertianMaterial", "Mesh", "NamedColour", "PhongMaterial", "Plane", "ReflectiveMaterial", "Scene", "SceneSpec",
-    "SmoothTransparentDialectric", "Sphere", "Spectrum", "load_obj",
+    "SmoothTransparentDialectric", "Sphere", "Spectrum", "load_obj", "DirectionalLight", "WhittedIntegrator",
 ]
 
 

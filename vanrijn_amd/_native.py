@@ -57,11 +57,24 @@ class ObjectDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("first", C.c_uint32), ("count", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class DirectionalLightC(C.Structure):
+    _fields_ = [("direction", Vec3), ("spectrum", Spectrum)]
+
+
+class IntegratorDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("light_count", C.c_uint32), ("ambient_light", Spectrum),
+                ("lights", C.POINTER(DirectionalLightC))]
+
+
+INTEGRATOR_SIMPLE_RANDOM, INTEGRATOR_WHITTED = 0, 1
+
+
 class SceneDesc(C.Structure):
     _fields_ = [("camera_location", Vec3), ("material_count", C.c_uint32), ("primitive_count", C.c_uint32),
                 ("mesh_count", C.c_uint32), ("object_count", C.c_uint32),
                 ("materials", C.POINTER(MaterialDesc)), ("primitives", C.POINTER(PrimitiveDesc)),
-                ("meshes", C.POINTER(MeshDesc)), ("objects", C.POINTER(ObjectDesc))]
+                ("meshes", C.POINTER(MeshDesc)), ("objects", C.POINTER(ObjectDesc)),
+                ("integrator", C.POINTER(IntegratorDesc))]
 
 
 class SceneInfo(C.Structure):

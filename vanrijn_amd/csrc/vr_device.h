@@ -610,6 +610,92 @@ __device__ __forceinline__ Best closest_hit(const DeviceScene& S, const RayPre& 
     return best;
 }
 
+// Sampler::sample(shadow ray).is_some() (whitted_integrator.rs:37-38): any object hit.  A
+// triangle counts when the exact line test passes on its own box (its leaf) and its test hits --
+// ancestors then pass too (superset boxes), so any tree may be walked; no distance ordering is
+// needed.  Uses the caller's LDS stack column (`st[depth * 256 + tid]`).
+template <int STACK>
+__device__ bool any_hit(const DeviceScene& S, const RayPre& p, uint32_t* st, int tid) {
+    for (int i = 0; i < S.prim_count; ++i) {
+        const Prim& pr = S.prims[i];
+        double d;
+        if (pr.kind == 0) {
+            if (plane_distance(pr, p, d)) return true;
+        } else if (sphere_distance(pr, p) >= 0.0) {
+            return true;
+        }
+    }
+    for (int b = 0; b < S.bvh_count; ++b) {
+        const Bvh& bvh = S.bvhs[b];
+        if (bvh.root == INT32_MIN) continue;
+        double lo, hi, bary[3];
+        if (!slab(bvh.root_box, p, lo, hi)) continue;
+        if (bvh.root < 0) {
+            if (triangle_distance(S.tris[~bvh.root], p, bary) >= 0.0) return true;
+            continue;
+        }
+        int sp = 0, node = bvh.root;
+        while (true) {
+            const Node& nd = S.nodes[node];
+            int next = -1;
+            for (int c = 0; c < 2; ++c) {
+                if (!slab(nd.box[c], p, lo, hi)) continue;
+                const int ch = nd.child[c];
+                if (ch < 0) {
+                    if (triangle_distance(S.tris[~ch], p, bary) >= 0.0) return true;
+                } else if (next < 0) {
+                    next = ch;
+                } else {
+                    st[sp * 256 + tid] = (uint32_t)ch;
+                    ++sp;
+                }
+            }
+            if (next >= 0) {
+                node = next;
+            } else if (sp > 0) {
+                --sp;
+                node = (int)st[sp * 256 + tid];
+            } else {
+                break;
+            }
+        }
+    }
+    return false;
+}
+
+// Material::bsdf as an affine map of the incoming intensity: out = a * I + b, for the
+// WhittedIntegrator's calls (bsdf(w_o, w_i, photon)); lambertian_material.rs:27-34,
+// reflective_material.rs:15-40, phong_material.rs:17-36, smooth_transparent_dialectric.rs:79-95
+__device__ __forceinline__ void bsdf_affine(const Material* m, V3 w_o, V3 w_i, double wl, double& a, double& b) {
+    b = 0.0;
+    if (m->kind == 1) {
+        if (w_i.z <= 0.0 || w_o.z <= 0.0) {
+            a = 0.0;
+            return;
+        }
+        const V3 refl = mk(-w_o.x, -w_o.y, w_o.z);
+        double c = dot(w_i, refl);
+        c = c < 0.0 ? 0.0 : (c > 1.0 ? 1.0 : c);
+        const double theta = acos(fabs(c));
+        const double sigma = 0.05, two = 2.0;
+        const double f = m->reflection * exp(-(pow(theta, two)) / (two * sigma * sigma));
+        a = (material_colour(m, wl) * m->diffuse) * (1.0 - f);
+        b = f;
+    } else if (m->kind == 2) {
+        if (w_i.z < 0.0 || w_o.z < 0.0) {
+            a = 0.0;
+            return;
+        }
+        const V3 refl = mk(-w_i.x, -w_i.y, w_i.z);
+        a = material_colour(m, wl) * m->diffuse;
+        b = pow(fabs(dot(w_o, refl)), m->smoothness) * (m->reflection / dot(w_i, mk(0.0, 0.0, 1.0)));
+    } else if (m->kind == 3) {
+        a = dielectric_strength(dielectric_fresnel(m, w_i, wl), w_o);
+    } else {
+        a = material_colour(m, wl) * m->diffuse;
+    }
+}
+
 __device__ __forceinline__ void hit_info(const DeviceScene& S, const Best& best, const RayPre& p, HitInfo& h) {
     if (best.kind == kPrim) {
         prim_info(S.prims[best.index], p, best.d, h);

@@ -281,6 +281,7 @@ struct vr_scene {
     std::vector<vr::Material> materials;
     std::vector<vr::Prim> prims;
     std::vector<vr::Bvh> bvhs;
+    std::vector<double> light_dirs;  // Whitted: 3 per light
     std::vector<vr::Node> nodes;
     std::vector<vr::Node32> nodes32;
     std::vector<vr::TriVerts> tris;
@@ -350,8 +351,9 @@ int upload(vr_scene* s) {
     const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
     const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
     size_t off[8], total = 0;
-    const size_t sizes[8] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh, 64 + vr::kCntCount * sizeof(unsigned long long),
-                             sz_nodes32};
+    const size_t sz_misc = 64 + vr::kCntCount * sizeof(unsigned long long);  // error flag, counters
+    const size_t sizes[8] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh,
+                             sz_misc + 3 * VR_MAX_LIGHTS * sizeof(double), sz_nodes32};
     for (int i = 0; i < 8; ++i) {
         off[i] = total;
         total += align_up<char>(std::max<size_t>(sizes[i], 1));
@@ -373,6 +375,10 @@ int upload(vr_scene* s) {
         VR_HIP(hipMemcpy(base + off[7], s->nodes32.data(), sz_nodes32, hipMemcpyHostToDevice));
     s->d_error = (int32_t*)(base + off[6]);
     s->d_counters = (unsigned long long*)(base + off[6] + 64);
+    s->dev.light_dirs = (const double*)(base + off[6] + sz_misc);
+    if (!s->light_dirs.empty())
+        VR_HIP(hipMemcpy(base + off[6] + sz_misc, s->light_dirs.data(), s->light_dirs.size() * sizeof(double),
+                         hipMemcpyHostToDevice));
     vr::DeviceScene& d = s->dev;
     d.nodes = (const vr::Node*)(base + off[0]);
     d.nodes32 = (const vr::Node32*)(base + off[7]);
@@ -579,6 +585,34 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         // the dielectric's strength at 0 nm is not its eta(0): a path cut at the recursion limit
         // (lambda 0) needs the general lambda-0 chain
         if (m.kind == VR_MATERIAL_DIELECTRIC) s->dark0 = false;
+    }
+    // integrator: Whitted's ambient and light spectra become extra material rows
+    if (desc->integrator && desc->integrator->kind == VR_INTEGRATOR_WHITTED) {
+        const vr_integrator_desc& ig = *desc->integrator;
+        if (ig.light_count > VR_MAX_LIGHTS || (ig.light_count && !ig.lights)) return bad("bad light list");
+        auto spectrum_row = [&](const vr_spectrum& sp, vr::Material& dm) {
+            if (sp.sample_count < 1 || sp.sample_count > VR_MAX_SPECTRUM_SAMPLES || !sp.samples) return false;
+            dm = vr::Material{};
+            dm.n = (int32_t)sp.sample_count;
+            dm.shortest = sp.shortest_wavelength;
+            dm.longest = sp.longest_wavelength;
+            std::memcpy(dm.samples, sp.samples, sizeof(double) * sp.sample_count);
+            return true;
+        };
+        s->dev.integrator = VR_INTEGRATOR_WHITTED;
+        s->dev.light_base = (int32_t)s->materials.size();
+        s->dev.light_count = (int32_t)ig.light_count;
+        vr::Material dm;
+        if (!spectrum_row(ig.ambient_light, dm)) return bad("ambient light spectrum needs 1..64 samples");
+        s->materials.push_back(dm);
+        for (uint32_t j = 0; j < ig.light_count; ++j) {
+            if (!spectrum_row(ig.lights[j].spectrum, dm)) return bad("light spectrum needs 1..64 samples");
+            s->materials.push_back(dm);
+            const vr_vec3& d = ig.lights[j].direction;
+            s->light_dirs.insert(s->light_dirs.end(), {d.x, d.y, d.z});
+        }
+    } else if (desc->integrator && desc->integrator->kind != VR_INTEGRATOR_SIMPLE_RANDOM) {
+        return bad("unknown integrator kind");
     }
     // objects: primitive lists keep their order; BVHs are built per mesh
     std::vector<int> mesh_object(desc->mesh_count, -1);

@@ -98,6 +98,14 @@ struct DeviceScene {
     double margin;         // distance-cull slack (absolute + relative), see DESIGN.md "Traversal"
     double behind_margin;  // cull of boxes entirely behind the origin
     double extent;         // max |coordinate| of camera and geometry (f32 box-test error bound)
+    // integrator: 0 SimpleRandomIntegrator (camera.rs:103), 1 WhittedIntegrator
+    // (whitted_integrator.rs:15-87): its ambient spectrum is materials[light_base], light j's
+    // spectrum materials[light_base + 1 + j], its direction light_dirs[3j..3j+2]
+    int32_t integrator;
+    int32_t light_count;
+    int32_t light_base;
+    int32_t pad_i;
+    const double* light_dirs;
 };
 
 struct RenderArgs {

@@ -82,7 +82,8 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3>
+// WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ uint32_t st_node[STACK * 256];
     const int tid = threadIdx.x;
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
     V3 ray_o = mk(0.0, 0.0, 0.0), ray_d = mk(0.0, 0.0, 1.0);  // next ray (state kRayReady)
+    double Wa = 0.0, Wb = 0.0;  // Whitted: the pending continuation's throughput and constant
 
     // BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
     auto culled = [&](double tlo, double thi) {
@@ -257,6 +259,33 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         }
         const V3 w_i = mk(dot(h.tangent, h.retro), dot(h.cotangent, h.retro), dot(h.normal, h.retro));
         const Material* mat = &S.materials[h.material];
+        if constexpr (WHITTED) {
+            // light terms, in order (fold from the camera photon's intensity 0): a shadow ray per
+            // light; blocked -> the ambient spectrum, else bsdf(W retro, W dir, light(lambda) |dir.n|)
+            double C = 0.0;
+            for (int j = 0; j < S.light_count; ++j) {
+                const V3 ldir = ldv(S.light_dirs + 3 * j);
+                const V3 d1 = normalize(ldir);
+                const RayPre sp = prepare(Ray{add(h.loc, scl(d1, kBounceBias)), normalize(d1)});
+                double term;
+                if (any_hit<STACK>(S, sp, st_node, tid)) {
+                    term = material_colour(&S.materials[S.light_base], lambda);
+                } else {
+                    const V3 wl = mk(dot(h.tangent, ldir), dot(h.cotangent, ldir), dot(h.normal, ldir));
+                    const double I = material_colour(&S.materials[S.light_base + 1 + j], lambda) * fabs(dot(ldir, h.normal));
+                    double ba, bb;
+                    bsdf_affine(mat, w_i, wl, lambda, ba, bb);
+                    term = ba * I + bb;
+                }
+                C = C + term;
+            }
+            Acc = Acc + T * C;
+            if (depth >= kRecursionLimit) {  // recursion_limit 0: the continuation contributes 0
+                flags |= 2;
+                finish(lambda, Acc);
+                return;
+            }
+        }
         V3 w_o;
         double pdf;
         // material kind: compiled in for the kinds the scene has (MATS 1: Lambertian only,
@@ -306,6 +335,19 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             wo_world.z = dot(inv2, w_o);
         }
         const double cosf = fabs(dot(wo_world, h.normal));
+        if constexpr (WHITTED) {
+            // continuation: bsdf(W retro, dir, L_next) |dir.n|, applied when its ray hits
+            double ba, bb;
+            bsdf_affine(mat, w_i, w_o, lambda, ba, bb);
+            Wa = (T * ba) * cosf;
+            Wb = (T * bb) * cosf;
+            const V3 d1 = normalize(wo_world);
+            ++bounces;
+            ray_o = add(h.loc, scl(d1, kBounceBias));
+            ray_d = normalize(d1);
+            state = kRayReady;
+            return;
+        }
         const double c_l = material_colour(mat, lambda);
         const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
         double a, a0, bterm;
@@ -373,7 +415,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
                 bool go = false;
-                if (depth < 0) {
+                if (WHITTED && depth >= 0) {
+                    if (!best.kind) {
+                        finish(lambda, Acc);  // the continuation missed: photon.scale_intensity(0)
+                    } else {
+                        Acc = Acc + Wb;
+                        T = Wa;
+                        depth += 1;
+                        go = true;
+                    }
+                } else if (depth < 0) {
                     if (!best.kind) {
                         finish(0.0, 0.0);  // camera ray missed: photon {0, 0} (camera.rs:110-113)
                     } else {
@@ -679,6 +730,21 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     mats = (mats == 1 || mats == 2) ? mats : 3;
     if (!dark0) mats = 3;  // the general kernel
     if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);  // experiment hook
+    if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
+        if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true, true, 3, 3, true>), grid, block, 0, s, a);
+        else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false, true, 3, 3, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3, 3, true>), grid, block, 0, s, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (mid) {
+            e = hipEventRecord(mid, s);
+            if (e != hipSuccess) return e;
+        }
+        const uint64_t npix = a.tile_width * a.tile_height;
+        hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
+                           (const double*)a.staging, npix, a.spp, a.accumulate);
+        return hipGetLastError();
+    }
 #define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \

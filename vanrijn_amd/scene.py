@@ -125,6 +125,22 @@ class SmoothTransparentDialectric:
         return SmoothTransparentDialectric(eta)
 
 
+# ------------------------------------------------------------------------------ integrators
+@dataclass
+class DirectionalLight:
+    """integrators/whitted_integrator.rs:10-13."""
+    direction: tuple
+    spectrum: Spectrum
+
+
+@dataclass
+class WhittedIntegrator:
+    """integrators/whitted_integrator.rs:15-87.  The reference's partial_render_scene always uses
+    SimpleRandomIntegrator (camera.rs:103); here a Scene may carry this one instead."""
+    ambient_light: Spectrum
+    lights: list
+
+
 # ------------------------------------------------------------------------------ geometry
 @dataclass
 class Plane:
@@ -217,6 +233,7 @@ class SceneSpec:
     materials: List[MaterialSpec]
     meshes: List[MeshSpec]
     objects: List[ObjectSpec]
+    integrator: object = None  # None (SimpleRandomIntegrator) or WhittedIntegrator
 
 
 class Scene:
@@ -225,9 +242,10 @@ class Scene:
     objects: list whose items are either a list of Plane/Sphere (a Vec<Box<dyn Primitive>>
     aggregate) or a BoundingVolumeHierarchy."""
 
-    def __init__(self, camera_location, objects):
+    def __init__(self, camera_location, objects, integrator=None):
         self.camera_location = tuple(float(c) for c in camera_location)
         self.objects = list(objects)
+        self.integrator = integrator
         self._spec = None
         self._device_scenes = {}
 
@@ -271,7 +289,7 @@ class Scene:
                         else:
                             raise TypeError(f"unsupported primitive {type(p).__name__}")
                     objs.append(ObjectSpec("primitives", prims))
-            self._spec = SceneSpec(self.camera_location, mats, meshes, objs)
+            self._spec = SceneSpec(self.camera_location, mats, meshes, objs, self.integrator)
         return self._spec
 
     def device_scene(self, device=0, host_only=False, device_bvh=False, reference_bvh=False):
@@ -315,8 +333,21 @@ class DeviceScene:
         prim_arr = (N.PrimitiveDesc * max(len(prims), 1))(*prims)
         obj_arr = (N.ObjectDesc * max(len(objs), 1))(*objs)
         mesh_arr = (N.MeshDesc * max(len(meshes), 1))(*meshes)
+        ig = None
+        if spec.integrator is not None:
+            def cspec(sp):
+                a = np.ascontiguousarray(sp.samples, dtype=np.float64)
+                keep.append(a)
+                return N.Spectrum(sp.shortest_wavelength, sp.longest_wavelength, a.size,
+                                  a.ctypes.data_as(C.POINTER(C.c_double)))
+            lights = (N.DirectionalLightC * max(len(spec.integrator.lights), 1))()
+            for j, li in enumerate(spec.integrator.lights):
+                lights[j] = N.DirectionalLightC(N.Vec3(*li.direction), cspec(li.spectrum))
+            keep.append(lights)
+            ig = N.IntegratorDesc(N.INTEGRATOR_WHITTED, len(spec.integrator.lights),
+                                  cspec(spec.integrator.ambient_light), lights)
         desc = N.SceneDesc(N.Vec3(*spec.camera_location), len(spec.materials), len(prims), len(meshes), len(objs),
-                           mats, prim_arr, mesh_arr, obj_arr)
+                           mats, prim_arr, mesh_arr, obj_arr, C.pointer(ig) if ig is not None else None)
         h = C.c_void_p()
         flags = ((N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0) |
                  (N.SCENE_REFERENCE_BVH if reference_bvh else 0))

@@ -21,7 +21,8 @@ import os
 import numpy as np
 
 from .scene import (BoundingVolumeHierarchy, ColourRgbF, LambertianMaterial, Mesh, NamedColour, PhongMaterial, Plane,
-                    ReflectiveMaterial, Scene, SmoothTransparentDialectric, Spectrum, Sphere, load_obj)
+                    ReflectiveMaterial, Scene, SmoothTransparentDialectric, Spectrum, Sphere, load_obj,
+                    DirectionalLight, WhittedIntegrator)
 
 CAMERA_LOCATION = (-2.0, 1.0, -5.0)  # main.rs:139, simple_scene.rs:25
 BUNNY_SHA256 = "7ee71a949c270c53226056a0ad120e8a8dcdba54d36c2420f987dd1cdd4e302f"
@@ -208,6 +209,17 @@ def materials_scene(mesh=None):
         ],
         BoundingVolumeHierarchy.build(bunny),
     ])
+
+
+def whitted_scene(mesh=None):
+    """materials_scene rendered with the WhittedIntegrator: two directional lights and an
+    ambient term (the reference ships no Whitted scene; this one exercises every material)."""
+    s = materials_scene(mesh)
+    warm = Spectrum.reflection_from_linear_rgb(ColourRgbF.new(1.0, 0.9, 0.7))
+    cool = Spectrum.reflection_from_linear_rgb(ColourRgbF.new(0.3, 0.4, 0.8))
+    s.integrator = WhittedIntegrator(Spectrum.grey(0.05), [DirectionalLight((0.4, 1.0, -0.3), warm),
+                                                           DirectionalLight((-0.6, 0.8, 0.2), cool)])
+    return s
 
 
 def synthetic_scene():
