@@ -220,7 +220,7 @@ struct Ray {
 };
 // Per-ray constants hoisted out of every box / triangle test (bit-identical to recomputing them)
 struct RayPre {
-    V3 o, d, inv;
+    V3 o, d;
     double sx, sy, pdz;
     int flags;  // bits 0-1: axis rotation r (permutation [r, r+1, r+2] mod 3); bit 2: exact_only
                 // (some |d_i| tiny or zero: every slab takes the division path); bit 3: behind_ok
@@ -236,7 +236,6 @@ __device__ __forceinline__ RayPre prepare(const Ray& r) {
     RayPre p;
     p.o = r.o;
     p.d = r.d;
-    p.inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
     // indices_with_index_of_largest_element_last (triangle.rs:108-122): signed comparisons;
     // the three outcomes [0,1,2], [1,2,0], [2,0,1] are the rotations r = 0, 1, 2
     int rot;
@@ -254,35 +253,10 @@ __device__ __forceinline__ RayPre prepare(const Ray& r) {
 }
 
 // raycasting/axis_aligned_bounding_box.rs:9-27 (+ util/interval.rs): the LINE slab test with
-// NaN-ignoring max/min.  The decision must equal the reference's division form bit for bit; the
-// common case is decided from reciprocal products (|error| <= ~3.3e-16 |t|) when the interval
-// is clearly non-empty or clearly empty, and only near-ties fall back to exact divisions.
-// Returns the (approximate) line interval for distance culling.
+// NaN-ignoring max/min, in the reference's division form (the exact decision).  Only called
+// where the f32 test cannot decide (slab32 == 2) and on the test-only / shadow-ray paths.
+// tlo / thi: the line interval, for distance culling.
 __device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& tlo, double& thi) {
-    double lo = -INFINITY, hi = INFINITY;
-    {
-        double a = (b[0] - p.o.x) * p.inv.x, c = (b[1] - p.o.x) * p.inv.x;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    {
-        double a = (b[2] - p.o.y) * p.inv.y, c = (b[3] - p.o.y) * p.inv.y;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    {
-        double a = (b[4] - p.o.z) * p.inv.z, c = (b[5] - p.o.z) * p.inv.z;
-        double mn = a > c ? c : a, mx = a > c ? a : c;
-        lo = fmax(lo, mn); hi = fmin(hi, mx);
-    }
-    tlo = lo;
-    thi = hi;
-    if (!p.exact_only()) {
-        double err = 1e-15 * (fabs(lo) + fabs(hi));
-        if (hi - lo > err) return true;
-        if (lo - hi > err) return false;
-    }
-    // exact reference form (divisions)
     double elo = -INFINITY, ehi = INFINITY;
     {
         double a = (b[0] - p.o.x) / p.d.x, c = (b[1] - p.o.x) / p.d.x;
@@ -299,10 +273,8 @@ __device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& t
         double mn = a > c ? c : a, mx = a > c ? a : c;
         elo = fmax(elo, mn); ehi = fmin(ehi, mx);
     }
-    if (p.exact_only()) {
-        tlo = elo;
-        thi = ehi;
-    }
+    tlo = elo;
+    thi = ehi;
     return !(elo > ehi);
 }
 
@@ -320,19 +292,21 @@ struct Ray32 {
 __device__ __forceinline__ Ray32 prepare32(const RayPre& p, double extent) {
     Ray32 r;
     r.ox = (float)p.o.x; r.oy = (float)p.o.y; r.oz = (float)p.o.z;
-    r.ix = (float)p.inv.x; r.iy = (float)p.inv.y; r.iz = (float)p.inv.z;
+    // correctly rounded f32 reciprocals of the f32 direction: within 1.2e-7 relative of 1/d
+    r.ix = 1.0f / (float)p.d.x; r.iy = 1.0f / (float)p.d.y; r.iz = 1.0f / (float)p.d.z;
     r.nx = -(r.ox * r.ix); r.ny = -(r.oy * r.iy); r.nz = -(r.oz * r.iz);
     // origins on the infinite plane can lie outside the scene extent: bound with |o| too
     const double big = fmax(extent, fmax(fmax(fabs(p.o.x), fabs(p.o.y)), fabs(p.o.z))) + 1.0;
-    const double m = fmax(fmax(fabs(p.inv.x), fabs(p.inv.y)), fabs(p.inv.z));
+    const double m = fmax(fmax(fabsf(r.ix), fabsf(r.iy)), fabsf(r.iz));
     const double ek = 6e-7 * big * m;
     r.ek = (p.exact_only() || !(ek < 1e30)) ? INFINITY : (float)ek;
     return r;
 }
 // Each slab value is one fused multiply-add per bound, two bounds per packed (v_pk_fma_f32)
 // instruction: t = RN(b32 * i32 - RN(o32 * i32)).  Its error against the exact (b - o) / d is at
-// most 1.2e-7 |t| + 2.4e-7 X |1/d| (outward-rounded bound 2^-23 |b|, f32 origin and reciprocal,
-// the product o * i and the fma each 2^-24), which E = ek + 2.4e-7 (|lo| + |hi|) covers twice.
+// most 1.8e-7 |t| + 2.4e-7 X |1/d| (reciprocal of the f32 direction 1.2e-7, fma 6e-8;
+// outward-rounded bound 2^-23 |b|, f32 origin and the product o * i 2^-24 each), which
+// E = ek + 3e-7 (|lo| + |hi|) covers (ek = 6e-7 X max |1/d|).
 typedef float vr_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo, float& thi) {
     const vr_f2 bx = {b[0], b[1]}, by = {b[2], b[3]}, bz = {b[4], b[5]};
@@ -341,7 +315,7 @@ __device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo
     const vr_f2 tz = __builtin_elementwise_fma(bz, (vr_f2){r.iz, r.iz}, (vr_f2){r.nz, r.nz});
     const float lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
     const float hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const float e = r.ek + 2.4e-7f * (fabsf(lo) + fabsf(hi));
+    const float e = r.ek + 3e-7f * (fabsf(lo) + fabsf(hi));
     tlo = lo - e;
     thi = hi + e;
     if (hi - lo > 2.0f * e) return 1;

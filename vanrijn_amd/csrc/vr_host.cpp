@@ -784,6 +784,18 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         s->node_count = s->nodes.size();
         s->tri_count = s->tris.size();
     }
+    // outward-rounded f32 root boxes (the kernel's pre-test)
+    for (auto& b : s->bvhs)
+        for (int k = 0; k < 6; ++k) {
+            const double v = b.root_box[k];
+            float f = (float)v;
+            if (k % 2 == 0) {
+                if ((double)f > v) f = std::nextafter(f, -INFINITY);
+            } else {
+                if ((double)f < v) f = std::nextafter(f, INFINITY);
+            }
+            b.root_box32[k] = f;
+        }
     // BVH objects in object order (ties across objects depend on it)
     std::sort(s->bvhs.begin(), s->bvhs.end(), [](const vr::Bvh& a, const vr::Bvh& b) { return a.object < b.object; });
     // f32 traversal copy: outward rounding keeps each f32 box a superset of its f64 box

@@ -77,6 +77,7 @@ struct Prim {
 
 struct Bvh {
     double root_box[6];  // bounds of the whole tree (tested first, as the reference's root)
+    float root_box32[6];  // the same, rounded outward to f32 (the slab32 pre-test)
     int32_t root;        // >= 0 interior node, < 0 leaf ~triangle, INT32_MIN: empty mesh
     int32_t object;      // scene object index
     int32_t tri_base;    // first triangle of this mesh in the global leaf-ordered arrays

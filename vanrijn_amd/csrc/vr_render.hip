@@ -168,9 +168,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             const Bvh& bvh = S.bvhs[bvh_i];
             if (bvh.root == INT32_MIN) continue;
             cur_object = bvh.object;
-            double lo, hi;
             if (COUNT) cnt.box_tests++;
-            if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
+            float flo, fhi;
+            const int rr = slab32(bvh.root_box32, pre32, flo, fhi);
+            if (rr == 0) continue;
+            if (rr == 1) {
+                if (flo > cull_far || fhi < cull_behind) continue;
+            } else {
+                double lo, hi;
+                if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
+            }
             if (bvh.root < 0) {  // a one-triangle BVH
                 test_tri(~bvh.root);
                 continue;
