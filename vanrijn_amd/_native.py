@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvanrijn_amd.so")
+# VR_LIBRARY: an alternative build for A/B timing (tools/ab.sh); the default is the in-tree library
+LIB_PATH = os.environ.get("VR_LIBRARY") or os.path.join(HERE, "lib", "libvanrijn_amd.so")
 
 VR_OK = 0
 STATUS = {
