@@ -103,7 +103,9 @@ def main():
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--scene", choices=["main", "bench"], default="main")
+    ap.add_argument("--scene", choices=["main", "bench", "c5"], default="main",
+                    help="main: main.rs scene (the headline); bench: benches/simple_scene.rs; "
+                         "c5: SURVEY 8(d) C5, main.rs's plane and spheres + the 1,051,392-triangle synthetic mesh")
     ap.add_argument("--mesh", default=None,
                     help="the reference's test_data/stanford_bunny.obj (size + sha256 verified) instead of the "
                          "procedural stand-in")
@@ -122,7 +124,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H, spp = args.width, args.height, args.spp
-    scene = scenes.main_scene(args.mesh) if args.scene == "main" else scenes.bench_scene(args.mesh)
+    if args.scene == "c5":
+        scene = scenes.synthetic_scene()
+    else:
+        scene = scenes.main_scene(args.mesh) if args.scene == "main" else scenes.bench_scene(args.mesh)
     dscene = scene.device_scene(local)
     info = dscene.info()
     tile = Tile(0, W, 0, H)
@@ -177,11 +182,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic: procedural bunny stand-in (69,312 triangles; the reference OBJ is an LFS pointer), "
+        "data": ("synthetic: lat-long displaced sphere mesh (1,051,392 triangles, seed 0x1DEA), counter-based RNG "
+                 "seed 0x5EED0001") if args.scene == "c5" else
+                ("synthetic: procedural bunny stand-in (69,312 triangles; the reference OBJ is an LFS pointer), "
                  "counter-based RNG seed 0x5EED0001") if args.mesh is None else
                 f"{os.path.basename(args.mesh)} (sha256-verified reference bunny), counter-based RNG seed 0x5EED0001",
-        "config": {"workload": f"main.rs scene (plane, 3 spheres, Lambertian bunny), {W}x{H} @{spp}spp per GPU"
-                               if args.scene == "main" else f"bench scene (reflective bunny), {W}x{H} @{spp}spp per GPU",
+        "config": {"workload": {"main": f"main.rs scene (plane, 3 spheres, Lambertian bunny), {W}x{H} @{spp}spp per GPU",
+                                "bench": f"bench scene (reflective bunny), {W}x{H} @{spp}spp per GPU",
+                                "c5": f"C5: main.rs plane + spheres + 1,051,392-triangle synthetic mesh, {W}x{H} "
+                                      f"@{spp}spp per GPU"}[args.scene],
                    "width": W, "height": H, "spp": spp, "triangles": info["triangle_count"],
                    "bvh_depth": info["max_bvh_depth"], "parallelism": f"spp-split x{world}, RCCL reduce"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

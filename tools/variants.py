@@ -28,7 +28,8 @@ def main():
                     help="NAME=v1,v2,... sweep over an environment variable (repeatable: cartesian product)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
-    scene = scenes.main_scene() if a.scene == "main" else scenes.bench_scene()
+    scene = {"main": scenes.main_scene, "bench": scenes.bench_scene, "c5": scenes.synthetic_scene,
+             "materials": scenes.materials_scene, "whitted": scenes.whitted_scene}[a.scene]()
     ds = scene.device_scene(0)
     W = H = a.size
     state = torch.zeros(W * H * 8, dtype=torch.float64, device="cuda")
