@@ -41,13 +41,31 @@ def stale():
 
 
 def build(force=False, verbose=False):
+    """Each source compiles to its own object in parallel (no device-side linking is needed: every
+    kernel is launched from its own translation unit), then one shared-library link."""
     if not force and not stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = [hipcc()] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-lz", "-o", LIB + ".tmp"]
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    if os.environ.get("VR_TUNING") == "1":  # the occupancy-variant kernels of tools/variants.py
+        compile_flags.append("-DVR_TUNING_VARIANTS")
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(LIB_DIR, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc()] + compile_flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-lz", "-o", LIB + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+        print(" ".join(link))
+    subprocess.check_call(link)
+    for o in objs:
+        os.remove(o)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

@@ -732,6 +732,7 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
+    (void)variant;
     // kinds present (bit 0 Lambertian, 1 reflective, 2 Phong or dielectric) -> specialisation:
     // Lambertian-only (1), reflective-only (2) or the general kernel (3)
     mats = (mats == 1 || mats == 2) ? mats : 3;
@@ -753,6 +754,7 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
         return hipGetLastError();
     }
 #define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)
+#ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
     else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
@@ -760,6 +762,12 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     else if (variant == 2) VR_LAUNCH(false, false, D, M, 2); \
     else if (variant == 4) VR_LAUNCH(false, false, D, M, 4); \
     else VR_LAUNCH(false, false, D, M, 3)
+#else
+#define VR_MODES(D, M)                                     \
+    if (recording) VR_LAUNCH(false, true, D, M, 3);        \
+    else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
+    else VR_LAUNCH(false, false, D, M, 3)
+#endif
     if (!dark0) {
         VR_MODES(false, 3);
     } else if (mats == 1) {
