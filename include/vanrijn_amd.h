@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 2
+#define VR_ABI_VERSION 3
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -168,6 +168,9 @@ typedef struct vr_scene_info {
     uint32_t object_count;
     double extent;           /* max |coordinate| of camera and geometry */
     uint64_t device_bytes;   /* scene bytes resident in HBM */
+    uint64_t wide_node_count;  /* nodes of the render kernel's 4-wide traversal tree (ABI 3) */
+    uint32_t traversal_stack;  /* deepest stack of the 4-wide walk, entries (ABI 3) */
+    uint32_t reserved;
 } vr_scene_info;
 int vr_scene_get_info(const vr_scene* scene, vr_scene_info* out);
 /* BVH leaf (in-order) sequence of mesh `mesh`: out[i] = input triangle index of leaf i. */

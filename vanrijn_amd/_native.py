@@ -80,7 +80,8 @@ class SceneDesc(C.Structure):
 
 class SceneInfo(C.Structure):
     _fields_ = [("triangle_count", C.c_uint64), ("node_count", C.c_uint64), ("max_bvh_depth", C.c_uint32),
-                ("object_count", C.c_uint32), ("extent", C.c_double), ("device_bytes", C.c_uint64)]
+                ("object_count", C.c_uint32), ("extent", C.c_double), ("device_bytes", C.c_uint64),
+                ("wide_node_count", C.c_uint64), ("traversal_stack", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class TileC(C.Structure):

@@ -185,21 +185,6 @@ __global__ void gather_kernel(const double* verts, const double* norms, const ui
     normals[pos] = tn;
 }
 
-// the f32 traversal copy: min bounds rounded toward -inf, max bounds toward +inf (the host
-// build's nextafter rule)
-__global__ void round_nodes_kernel(const Node* nodes, uint64_t n, Node32* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Node nd = nodes[i];
-    Node32 m;
-    for (int c = 0; c < 2; ++c) {
-        for (int k = 0; k < 6; ++k) m.box[c][k] = (k & 1) ? __double2float_ru(nd.box[c][k]) : __double2float_rd(nd.box[c][k]);
-        m.child[c] = nd.child[c];
-    }
-    m.pad[0] = m.pad[1] = 0;
-    out[i] = m;
-}
-
 }  // namespace build
 
 #define VRB(call)                                 \
@@ -328,14 +313,6 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
     VRB(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < n; ++i) leaf_order[i] = p[i];
     return 0;
-}
-
-int device_round_nodes(const Node* nodes, uint64_t n, Node32* out, void* stream) {
-    if (n == 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(build::round_nodes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, n,
-                       out);
-    return (int)hipGetLastError();
 }
 
 }  // namespace vr

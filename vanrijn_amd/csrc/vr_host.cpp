@@ -268,6 +268,91 @@ struct SahBuilder {
     }
 };
 
+// f32 copies of f64 box bounds, rounded outward (a lower bound down, an upper bound up), so an
+// f32 box contains its f64 box
+float round_lower(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+float round_upper(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+// The render kernel's 4-wide tree, collapsed from a binary tree (the SAH traversal tree, or the
+// reference's median-split tree): starting from a binary node's two children, the interior child
+// with the largest surface area is replaced by its two children until there are four (or only
+// leaves).  Leaf children keep the triangle's own box, so DESIGN.md section 5's argument carries
+// over unchanged: interior boxes are unions (supersets), and a triangle is tested iff the exact
+// line test passes on its own box.  `stack` is the deepest the kernel's traversal stack can get
+// (a visit pushes all but one hit interior child): the maximum over root-to-node paths of the
+// sum of (interior children - 1).
+struct WideBuilder {
+    const std::vector<vr::Node>& bin;
+    std::vector<vr::Node4>& n4;
+    std::vector<vr::Node4x>& n4x;
+    int stack = 0;
+    WideBuilder(const std::vector<vr::Node>& b, std::vector<vr::Node4>& a, std::vector<vr::Node4x>& x)
+        : bin(b), n4(a), n4x(x) {}
+
+    static double area(const double* b) {
+        const double dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
+        if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+        return dx * dy + dy * dz + dz * dx;
+    }
+
+    // wide node over binary interior node `b`; `pushed`: stack entries held by its ancestors
+    int32_t collapse(int32_t b, int pushed) {
+        int32_t code[4];
+        const double* box[4];
+        int n = 2;
+        for (int c = 0; c < 2; ++c) {
+            code[c] = bin[b].child[c];
+            box[c] = bin[b].box[c];
+        }
+        while (n < 4) {
+            int pick = -1;
+            double best = -1.0;
+            for (int k = 0; k < n; ++k)
+                if (code[k] >= 0 && area(box[k]) > best) {
+                    best = area(box[k]);
+                    pick = k;
+                }
+            if (pick < 0) break;
+            const vr::Node& c = bin[code[pick]];
+            code[pick] = c.child[0];
+            box[pick] = c.box[0];
+            code[n] = c.child[1];
+            box[n] = c.box[1];
+            ++n;
+        }
+        const int32_t me = (int32_t)n4.size();
+        n4.emplace_back();
+        n4x.emplace_back();
+        int interior = 0;
+        for (int k = 0; k < n; ++k) interior += code[k] >= 0;
+        const int here = pushed + std::max(0, interior - 1);
+        stack = std::max(stack, here);
+        int32_t out[4];
+        for (int k = 0; k < 4; ++k) out[k] = vr::kEmptyChild;
+        for (int k = 0; k < n; ++k) out[k] = code[k] >= 0 ? collapse(code[k], here) : code[k];
+        vr::Node4& w = n4[me];
+        vr::Node4x& x = n4x[me];
+        std::memset(&w, 0, sizeof w);
+        for (int k = 0; k < 4; ++k) {
+            w.child[k] = out[k];
+            for (int j = 0; j < 6; ++j) {
+                const double v = k < n ? box[k][j] : NAN;
+                x.box[k][j] = v;
+                w.box[k][j] = k < n ? ((j & 1) ? round_upper(v) : round_lower(v)) : NAN;
+            }
+        }
+        return me;
+    }
+};
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -283,7 +368,9 @@ struct vr_scene {
     std::vector<vr::Bvh> bvhs;
     std::vector<double> light_dirs;  // Whitted: 3 per light
     std::vector<vr::Node> nodes;
-    std::vector<vr::Node32> nodes32;
+    std::vector<vr::Node4> nodes4;  // the render kernel's 4-wide tree (collapse_wide)
+    std::vector<vr::Node4x> nodes4x;
+    int wide_stack = 0;             // deepest traversal stack of the 4-wide tree
     std::vector<vr::TriVerts> tris;
     std::vector<vr::TriNormals> normals;
     std::vector<std::vector<uint64_t>> leaf_order;  // per mesh
@@ -291,7 +378,7 @@ struct vr_scene {
     int max_depth = 0;
     uint32_t object_count = 0;
     // VR_SCENE_DEVICE_BVH: the meshes' BVHs are built on the device after upload (host vectors
-    // nodes / nodes32 / tris / normals stay empty; the counts below size the device arrays)
+    // nodes / tris / normals stay empty; the counts below size the device arrays)
     bool device_bvh = false;
     uint64_t node_count = 0, tri_count = 0;
     struct PendingMesh {
@@ -325,7 +412,17 @@ struct vr_scene {
 
 namespace {
 
-int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }
+int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }  // binary tree walks
+int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render kernel (+1: branchless pushes)
+
+// the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
+void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
+    s->nodes4.clear();
+    s->nodes4x.clear();
+    WideBuilder W(nodes, s->nodes4, s->nodes4x);
+    for (auto& b : s->bvhs) b.root4 = b.root >= 0 ? W.collapse(b.root, 0) : b.root;
+    s->wide_stack = W.stack;
+}
 
 template <class T>
 size_t align_up(size_t v) {
@@ -344,17 +441,20 @@ struct CallScratch {
 int upload(vr_scene* s) {
     VR_HIP(hipSetDevice(s->device));
     const size_t sz_nodes = s->node_count * sizeof(vr::Node);
-    const size_t sz_nodes32 = s->node_count * sizeof(vr::Node32);
+    // the 4-wide tree has at most one node per binary interior node (device builds collapse after
+    // the build, so its arrays are sized by that bound)
+    const size_t sz_nodes4 = s->node_count * sizeof(vr::Node4);
+    const size_t sz_nodes4x = s->node_count * sizeof(vr::Node4x);
     const size_t sz_tris = s->tri_count * sizeof(vr::TriVerts);
     const size_t sz_norm = s->tri_count * sizeof(vr::TriNormals);
     const size_t sz_mat = s->materials.size() * sizeof(vr::Material);
     const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
     const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
-    size_t off[8], total = 0;
+    size_t off[9], total = 0;
     const size_t sz_misc = 64 + vr::kCntCount * sizeof(unsigned long long);  // error flag, counters
-    const size_t sizes[8] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh,
-                             sz_misc + 3 * VR_MAX_LIGHTS * sizeof(double), sz_nodes32};
-    for (int i = 0; i < 8; ++i) {
+    const size_t sizes[9] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh,
+                             sz_misc + 3 * VR_MAX_LIGHTS * sizeof(double), sz_nodes4, sz_nodes4x};
+    for (int i = 0; i < 9; ++i) {
         off[i] = total;
         total += align_up<char>(std::max<size_t>(sizes[i], 1));
     }
@@ -367,12 +467,10 @@ int upload(vr_scene* s) {
     const void* src[6] = {s->nodes.data(), s->tris.data(), s->normals.data(), s->materials.data(), s->prims.data(),
                           s->bvhs.data()};
     for (int i = 0; i < 6; ++i) {
-        if (s->device_bvh && i < 3) continue;  // filled by the device build below
+        if (s->device_bvh && (i < 3 || i == 5)) continue;  // filled by the device build below
         if (sizes[i]) VR_HIP(hipMemcpy(base + off[i], src[i], sizes[i], hipMemcpyHostToDevice));
     }
     VR_HIP(hipMemset(base + off[6], 0, sizes[6]));
-    if (sz_nodes32 && !s->device_bvh)
-        VR_HIP(hipMemcpy(base + off[7], s->nodes32.data(), sz_nodes32, hipMemcpyHostToDevice));
     s->d_error = (int32_t*)(base + off[6]);
     s->d_counters = (unsigned long long*)(base + off[6] + 64);
     s->dev.light_dirs = (const double*)(base + off[6] + sz_misc);
@@ -381,7 +479,8 @@ int upload(vr_scene* s) {
                          hipMemcpyHostToDevice));
     vr::DeviceScene& d = s->dev;
     d.nodes = (const vr::Node*)(base + off[0]);
-    d.nodes32 = (const vr::Node32*)(base + off[7]);
+    d.nodes4 = (const vr::Node4*)(base + off[7]);
+    d.nodes4x = (const vr::Node4x*)(base + off[8]);
     d.tris = (const vr::TriVerts*)(base + off[1]);
     d.normals = (const vr::TriNormals*)(base + off[2]);
     d.materials = (const vr::Material*)(base + off[3]);
@@ -403,10 +502,18 @@ int upload(vr_scene* s) {
                                                     hipGetErrorString((hipError_t)e));
             s->max_depth = std::max(s->max_depth, levels);
         }
-        const int e = vr::device_round_nodes(nodes, s->node_count, (vr::Node32*)(base + off[7]), cs.stream);
-        if (e) return fail(VR_ERROR_DEVICE, "device node rounding failed");
         VR_HIP(hipStreamSynchronize(cs.stream));
         s->pending.clear();  // the caller's arrays are not kept
+        // the 4-wide traversal tree: collapsed on the host from the device-built nodes
+        std::vector<vr::Node> bin(s->node_count);
+        if (sz_nodes) VR_HIP(hipMemcpy(bin.data(), nodes, sz_nodes, hipMemcpyDeviceToHost));
+        collapse_wide(s, bin);
+        if (sz_bvh) VR_HIP(hipMemcpy(base + off[5], s->bvhs.data(), sz_bvh, hipMemcpyHostToDevice));
+    }
+    if (!s->nodes4.empty()) {
+        VR_HIP(hipMemcpy(base + off[7], s->nodes4.data(), s->nodes4.size() * sizeof(vr::Node4), hipMemcpyHostToDevice));
+        VR_HIP(hipMemcpy(base + off[8], s->nodes4x.data(), s->nodes4x.size() * sizeof(vr::Node4x),
+                         hipMemcpyHostToDevice));
     }
     return VR_OK;
 }
@@ -419,7 +526,8 @@ int check_render_params(const vr_scene* s, const vr_render_params* p) {
     if (t.end_column < t.start_column || t.end_row < t.start_row || t.end_column > p->width ||
         t.end_row > p->height || p->width == 0 || p->height == 0)
         return fail(VR_ERROR_INVALID_ARGUMENT, "tile outside the image");
-    if (stack_depth(s) > 48) return fail(VR_ERROR_UNSUPPORTED, "BVH deeper than the largest traversal stack (48)");
+    if (stack_depth(s) > 48 || wide_stack_depth(s) > 48)
+        return fail(VR_ERROR_UNSUPPORTED, "BVH deeper than the largest traversal stack (48)");
     return VR_OK;
 }
 
@@ -786,38 +894,11 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     }
     // outward-rounded f32 root boxes (the kernel's pre-test)
     for (auto& b : s->bvhs)
-        for (int k = 0; k < 6; ++k) {
-            const double v = b.root_box[k];
-            float f = (float)v;
-            if (k % 2 == 0) {
-                if ((double)f > v) f = std::nextafter(f, -INFINITY);
-            } else {
-                if ((double)f < v) f = std::nextafter(f, INFINITY);
-            }
-            b.root_box32[k] = f;
-        }
+        for (int k = 0; k < 6; ++k) b.root_box32[k] = (k % 2 == 0) ? round_lower(b.root_box[k]) : round_upper(b.root_box[k]);
     // BVH objects in object order (ties across objects depend on it)
     std::sort(s->bvhs.begin(), s->bvhs.end(), [](const vr::Bvh& a, const vr::Bvh& b) { return a.object < b.object; });
-    // f32 traversal copy: outward rounding keeps each f32 box a superset of its f64 box
-    s->nodes32.resize(s->nodes.size());
-    for (size_t i = 0; i < s->nodes.size(); ++i) {
-        const vr::Node& n = s->nodes[i];
-        vr::Node32& m = s->nodes32[i];
-        std::memset(&m, 0, sizeof m);
-        for (int c = 0; c < 2; ++c) {
-            for (int k = 0; k < 6; ++k) {
-                const double v = n.box[c][k];
-                float f = (float)v;
-                if (k % 2 == 0) {
-                    if ((double)f > v) f = std::nextafter(f, -INFINITY);
-                } else {
-                    if ((double)f < v) f = std::nextafter(f, INFINITY);
-                }
-                m.box[c][k] = f;
-            }
-            m.child[c] = n.child[c];
-        }
-    }
+    // the render kernel's 4-wide tree (device builds: after the build, in upload)
+    if (!s->device_bvh) collapse_wide(s, s->nodes);
     s->extent = extent;
     vr::DeviceScene& d = s->dev;
     d.prim_count = (int32_t)s->prims.size();
@@ -861,6 +942,9 @@ int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     out->object_count = s->object_count;
     out->extent = s->extent;
     out->device_bytes = s->device_bytes;
+    out->wide_node_count = s->nodes4.size();
+    out->traversal_stack = (uint32_t)s->wide_stack;
+    out->reserved = 0;
     return VR_OK;
 }
 
@@ -939,7 +1023,9 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
             if (!start || !mid) return fail(VR_ERROR_DEVICE, "hipEventCreate failed");
             VR_HIP(hipEventRecord(start, st));
         }
-        int lr = vr::launch_render(a, stack_depth(s), counting, recording, s->dark0, s->mats ? s->mats : 3,
+        // LDS stack entries: the 4-wide walk's, and the binary walk's for Whitted shadow rays
+        const int stack = s->dev.integrator == 1 ? std::max(stack_depth(s), wide_stack_depth(s)) : wide_stack_depth(s);
+        int lr = vr::launch_render(a, stack, counting, recording, s->dark0, s->mats ? s->mats : 3,
                                     std::max(1, s->cu_count) * 3, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {

@@ -25,16 +25,25 @@ struct alignas(128) Node {
 };
 static_assert(sizeof(Node) == 128, "Node must be one 128-B line");
 
-// The traversal copy of a Node: child boxes rounded OUTWARD to f32 (so each f32 box contains
-// its f64 box), same child links, 64 B.  The bunny BVH fits one XCD's 4 MB L2 in this form.
-// A box test is decided from it unless the f32 interval is within its error bound of a tie, in
-// which case the exact f64 box of the same index (Node) is fetched.
-struct alignas(64) Node32 {
-    float box[2][6];   // 48 B
-    int32_t child[2];  //  8 B
-    int32_t pad[2];    //  8 B -> 64 B
+// The traversal tree the render kernel walks: a 4-wide BVH collapsed from the binary traversal
+// tree (the reference's closest hit does not depend on the tree's shape), so
+// a ray's chain of dependent node fetches is about half as long as in the binary tree.  Child
+// boxes are rounded OUTWARD to f32 (each f32 box contains its f64 box); child[c] >= 0: wide node
+// index, child[c] < 0 (and != kEmptyChild): leaf holding triangle ~child[c], whose box is the
+// triangle's own box; kEmptyChild: unused slot.  A box test is decided from this record unless
+// the f32 interval is within its error bound of a tie; then the exact f64 box of the same slot
+// (Node4x, same index) decides.
+constexpr int32_t kEmptyChild = INT32_MIN;  // ~INT32_MAX: never a triangle (tri_count <= INT32_MAX)
+struct alignas(128) Node4 {
+    float box[4][6];   // 96 B: {min x, max x, min y, max y, min z, max z} per child
+    int32_t child[4];  // 16 B
+    int32_t pad[4];    // 16 B -> 128 B, one cache line
 };
-static_assert(sizeof(Node32) == 64, "Node32 must be 64 B");
+static_assert(sizeof(Node4) == 128, "Node4 must be one 128-B line");
+struct alignas(64) Node4x {
+    double box[4][6];  // 192 B: the exact boxes (read only for f32 tests too close to call)
+};
+static_assert(sizeof(Node4x) == 192, "Node4x must be 192 B");
 
 // Triangle vertices in traversal-BVH leaf order, 80 B for 16-B aligned loads.  `rank` is the
 // triangle's scene-wide position in the REFERENCE tree's in-order leaf sequence (tri_base + leaf
@@ -79,6 +88,8 @@ struct Bvh {
     double root_box[6];  // bounds of the whole tree (tested first, as the reference's root)
     float root_box32[6];  // the same, rounded outward to f32 (the slab32 pre-test)
     int32_t root;        // >= 0 interior node, < 0 leaf ~triangle, INT32_MIN: empty mesh
+    int32_t root4;       // the same in the 4-wide tree (>= 0: Node4 index)
+    int32_t pad_b;
     int32_t object;      // scene object index
     int32_t tri_base;    // first triangle of this mesh in the global leaf-ordered arrays
     int32_t material;
@@ -86,8 +97,9 @@ struct Bvh {
 
 // Device view of a scene (all pointers are device pointers on one GPU).
 struct DeviceScene {
-    const Node* nodes;
-    const Node32* nodes32;
+    const Node* nodes;     // binary tree (trace / shadow rays)
+    const Node4* nodes4;   // 4-wide traversal tree (render kernel)
+    const Node4x* nodes4x;
     const TriVerts* tris;
     const TriNormals* normals;
     const Material* materials;
@@ -172,7 +184,6 @@ int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rg
 int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
                      Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
                      int* levels, void* stream);
-int device_round_nodes(const Node* nodes, uint64_t n, Node32* out, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

@@ -23,6 +23,7 @@
 //     the reference's Kahan update_pixel, so the buffers are bit-identical to sequential calls.
 #include <hip/hip_runtime.h>
 
+#include <float.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -78,6 +79,8 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
 
 // kRayReady: the lane's next ray (ray_o, ray_d) is set and begin_ray runs once for all such
 // lanes at the end of phase A (one inlined copy for bounce and camera rays alike)
+constexpr int kPend = 8;  // pending leaf triangles per lane (LDS)
+
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
@@ -86,6 +89,10 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ uint32_t st_node[STACK * 256];
+    // leaf triangles met during traversal wait here for a leaf round, in which every lane with
+    // one tests it: the f64 triangle test then runs for many lanes at once instead of for the few
+    // that reached a leaf in this step.  [slot][thread], LIFO, kPend slots per lane.
+    __shared__ int32_t st_pend[kPend * 256];
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
     const DeviceScene& S = A.scene;
@@ -119,10 +126,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     Ray32 pre32;
     Best best;
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
-    // leaf triangles met during traversal wait here (p0 first) for a leaf round, in which every
-    // lane with one tests it: the f64 triangle test then runs for many lanes at once instead of
-    // for the few that reached a leaf in this step
-    int np = 0, p0 = -1, p1 = -1, p2 = -1, p3 = -1;
+    int np = 0;  // pending leaf triangles in st_pend
     // f32 forms of the cull thresholds: cull_far >= bound + margin (rounded up), cull_behind <=
     // -behind_margin (rounded down; -inf when behind-culling is off) -- never tighter than f64
     float cull_far = INFINITY, cull_behind = -INFINITY;
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     auto start_bvhs = [&]() {
         for (; bvh_i < S.bvh_count; ++bvh_i) {
             const Bvh& bvh = S.bvhs[bvh_i];
-            if (bvh.root == INT32_MIN) continue;
+            if (bvh.root4 == INT32_MIN) continue;
             cur_object = bvh.object;
             if (COUNT) cnt.box_tests++;
             float flo, fhi;
@@ -178,11 +182,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
                 double lo, hi;
                 if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
             }
-            if (bvh.root < 0) {  // a one-triangle BVH
-                test_tri(~bvh.root);
+            if (bvh.root4 < 0) {  // a one-triangle BVH
+                test_tri(~bvh.root4);
                 continue;
             }
-            node = bvh.root;
+            node = bvh.root4;
             sp = 0;
             return true;
         }
@@ -536,55 +540,72 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
         do {
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             VR_STAMP(5);
-            // node step: lanes with room for two more pending leaves
-            if (state == kTraversing && node >= 0 && np <= 2) {
-                const Node32& nd = S.nodes32[node];
-                if (COUNT) { cnt.node_visits++; cnt.box_tests += 2; }
-                const int c0 = nd.child[0], c1 = nd.child[1];
-                float f0, g0, f1, g1;
-                const int r0 = slab32(nd.box[0], pre32, f0, g0);
-                const int r1 = slab32(nd.box[1], pre32, f1, g1);
-                bool h0 = r0 == 1 && !(f0 > cull_far || g0 < cull_behind);
-                bool h1 = r1 == 1 && !(f1 > cull_far || g1 < cull_behind);
-                if (r0 == 2 || r1 == 2) { VR_SEC(2); }
+            // node step (4-wide node): lanes with room for four more pending leaves
+            if (state == kTraversing && node >= 0 && np <= kPend - 4) {
+                const Node4& nd = S.nodes4[node];
+                if (COUNT) cnt.node_visits++;
+                int c[4];
+                float f[4];
+                uint32_t hm = 0, xm = 0;  // per-child bits: hit (decided in f32), too close to call
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    c[k] = nd.child[k];
+                    float g;
+                    const int r = slab32(nd.box[k], pre32, f[k], g);
+                    const bool live = c[k] != kEmptyChild;
+                    if (COUNT && live) cnt.box_tests++;
+                    hm |= (live && r == 1 && !(f[k] > cull_far || g < cull_behind)) ? 1u << k : 0u;
+                    xm |= (live && r == 2) ? 1u << k : 0u;
+                }
+                if (xm) { VR_SEC(2); }
                 // too close to call in f32: the exact test and the f64 cull, one inlined copy
                 // run once per undecided child
-                bool x0 = r0 == 2, x1 = r1 == 2;
-                while (x0 || x1) {
-                    const int c = x0 ? 0 : 1;
+                while (xm) {
+                    const int k = __builtin_ctz(xm);
+                    xm &= xm - 1;
                     if (COUNT) cnt.exact_boxes++;
                     double lo, hi;
-                    const bool h = slab(S.nodes[node].box[c], pre, lo, hi) && !culled(lo, hi);
-                    if (c == 0) { h0 = h; x0 = false; } else { h1 = h; x1 = false; }
+                    if (slab(S.nodes4x[node].box[k], pre, lo, hi) && !culled(lo, hi)) hm |= 1u << k;
                 }
-                // leaf: queue its triangle (selects, not stores through a pointer to the slot:
-                // that would demote p0..p3 to scratch memory)
-                if (h0 && c0 < 0) {
-                    const int t = ~c0;
-                    p2 = np == 2 ? t : p2;
-                    p1 = np == 1 ? t : p1;
-                    p0 = np == 0 ? t : p0;
-                    ++np;
-                    h0 = false;
+                // leaf children: queue their triangles (unconditional LDS writes, the count
+                // advances only for hits; np <= kPend - 4 leaves room for all four)
+                float key[4];
+                int ch[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool h = (hm >> k) & 1u;
+                    st_pend[np * 256 + tid] = ~c[k];
+                    np += (h && c[k] < 0) ? 1 : 0;
+                    // hit: a finite key (NaN or infinite f32 bounds of exactly-decided children
+                    // clamp into range); INFINITY marks "not descended"
+                    key[k] = (h && c[k] >= 0) ? fminf(fmaxf(f[k], -FLT_MAX), FLT_MAX) : INFINITY;
+                    ch[k] = c[k];
                 }
-                if (h1 && c1 < 0) {
-                    const int t = ~c1;
-                    p3 = np == 3 ? t : p3;
-                    p2 = np == 2 ? t : p2;
-                    p1 = np == 1 ? t : p1;
-                    p0 = np == 0 ? t : p0;
-                    ++np;
-                    h1 = false;
-                }
-                if (h0 && h1) {
-                    const bool swap = f1 < f0;  // near child first
-                    st_node[sp * 256 + tid] = (uint32_t)(swap ? c0 : c1);
-                    ++sp;
-                    node = swap ? c1 : c0;
-                } else if (h0) {
-                    node = c0;
-                } else if (h1) {
-                    node = c1;
+                // interior children near-first: sorting network on (entry distance, child)
+                auto cas = [&](int i, int j) {
+                    const bool sw = key[j] < key[i];
+                    const float ki = key[i], kj = key[j];
+                    const int ci = ch[i], cj = ch[j];
+                    key[i] = sw ? kj : ki;
+                    key[j] = sw ? ki : kj;
+                    ch[i] = sw ? cj : ci;
+                    ch[j] = sw ? ci : cj;
+                };
+                cas(0, 1);
+                cas(2, 3);
+                cas(0, 2);
+                cas(1, 3);
+                cas(1, 2);
+                if (key[0] < INFINITY) {
+                    // farthest first, so the nearest remaining pops first (writes at sp are
+                    // unconditional: the stack holds one spare entry)
+                    st_node[sp * 256 + tid] = (uint32_t)ch[3];
+                    sp += key[3] < INFINITY ? 1 : 0;
+                    st_node[sp * 256 + tid] = (uint32_t)ch[2];
+                    sp += key[2] < INFINITY ? 1 : 0;
+                    st_node[sp * 256 + tid] = (uint32_t)ch[1];
+                    sp += key[1] < INFINITY ? 1 : 0;
+                    node = ch[0];
                 } else if (sp > 0) {
                     --sp;
                     node = (int)st_node[sp * 256 + tid];
@@ -596,17 +617,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
             // stalled on theirs
             const uint64_t pm = __ballot(np > 0);
             if (pm != 0) {
-                const bool stalled = np > 0 && (node < 0 || np > 2);
+                const bool stalled = np > 0 && (node < 0 || np > kPend - 4);
                 const uint64_t stm = __ballot(stalled);
                 if (__popcll(pm) >= (int)A.leaf_threshold || __popcll(stm) >= (int)A.leaf_stall ||
-                    __ballot(state == kTraversing && node >= 0 && np <= 2) == 0) {
+                    __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
                     if (np > 0) {
                         VR_SEC(0);
-                        test_tri(p0);
-                        p0 = p1;
-                        p1 = p2;
-                        p2 = p3;
                         --np;
+                        test_tri(st_pend[np * 256 + tid]);
                     }
                 }
             }
