@@ -87,7 +87,12 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
-__global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
+// The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
+// restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
+// reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
+__global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const Prim* __restrict__ g_prims,
+                                                           const Material* __restrict__ g_materials,
+                                                           const Bvh* __restrict__ g_bvhs) {
     __shared__ uint32_t st_node[STACK * 256];
     // leaf triangles met during traversal wait here for a leaf round, in which every lane with
     // one tests it: the f64 triangle test then runs for many lanes at once instead of for the few
@@ -95,7 +100,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A) {
     __shared__ int32_t st_pend[kPend * 256];
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
-    const DeviceScene& S = A.scene;
+    DeviceScene S = A.scene;
+    S.prims = g_prims;
+    S.materials = g_materials;
+    S.bvhs = g_bvhs;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t sec[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define VR_SEC(i) \
@@ -757,9 +765,9 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     if (!dark0) mats = 3;  // the general kernel
     if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);  // experiment hook
     if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
-        if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true, true, 3, 3, true>), grid, block, 0, s, a);
-        else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false, true, 3, 3, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3, 3, true>), grid, block, 0, s, a);
+        if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
+        else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
+        else hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (mid) {
@@ -771,7 +779,9 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
                            (const double*)a.staging, npix, a.spp, a.accumulate);
         return hipGetLastError();
     }
-#define VR_LAUNCH(C, R, D, M, W) hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a)
+#define VR_LAUNCH(C, R, D, M, W)                                                                      \
+    hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a, a.scene.prims, \
+                       a.scene.materials, a.scene.bvhs)
 #ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
