@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vanrijn_amd import scenes  # noqa: E402
 from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
 
-SECTIONS = ["shade", "refill", "camera_begin_ray", "node_step", "leaf_tests", "stack_loop"]
+SECTIONS = ["shade", "refill", "camera_begin_ray", "node_step", "leaf_round", "next_bvh_and_loop"]
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 which = sys.argv[2] if len(sys.argv) > 2 else "main"
 torch.cuda.set_device(0)

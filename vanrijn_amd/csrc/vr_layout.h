@@ -168,7 +168,7 @@ enum Counter : int {
     kCntOuterSlots = 7,      // 64 x wave-level path-loop iterations
     kCntExactBoxes = 8,      // f32 box tests that fell back to the exact f64 test
     kCntCycles = 9,          // 9..14: wave clock cycles per section (diagnostic, VR_COUNTERS_PATH):
-                             // shade, refill, camera + begin_ray, -, -, traversal + loop
+                             // shade, refill, camera + begin_ray, node step, leaf round, next BVH + loop
     kCntSections = 15,       // 15..23: wave-level executions of code sections (diagnostic):
                              // leaf test, 2nd leaf test, exact box, shade, camera, begin_ray,
                              // finish, refill, start_bvhs in traversal

@@ -77,7 +77,7 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
     return per_chunk * (chunk_rounds(a) + tail_of(a));
 }
 
-// kRayReady: the lane's next ray (ray_o, ray_d) is set and begin_ray runs once for all such
+// kRayReady: the lane's next ray (pre.o, pre.d) is set and begin_ray runs once for all such
 // lanes at the end of phase A (one inlined copy for bounce and camera rays alike)
 constexpr int kPend = 8;  // pending leaf triangles per lane (LDS)
 
@@ -140,7 +140,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     float cull_far = INFINITY, cull_behind = -INFINITY;
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
-    V3 ray_o = mk(0.0, 0.0, 0.0), ray_d = mk(0.0, 0.0, 1.0);  // next ray (state kRayReady)
     double Wa = 0.0, Wb = 0.0;  // Whitted: the pending continuation's throughput and constant
 
     // BVH cull: subtree entirely beyond the closest hit (+margin) or behind the origin
@@ -200,9 +199,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         }
         return false;
     };
-    // a new ray (directions already normalised): primitive lists first, then the BVHs
-    auto begin_ray = [&](V3 o, V3 d) {
-        pre = prepare(Ray{o, d});
+    // the lane's next ray, already in pre.o / pre.d (directions normalised; the next ray is kept
+    // there, not in registers of its own that would stay live through the traversal phase):
+    // primitive lists first, then the BVHs
+    auto begin_ray = [&]() {
+        pre = prepare(Ray{pre.o, pre.d});
         pre32 = prepare32(pre, S.extent);
         if (COUNT) cnt.rays++;
         best.kind = kNone;
@@ -362,8 +363,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             Wb = (T * bb) * cosf;
             const V3 d1 = normalize(wo_world);
             ++bounces;
-            ray_o = add(h.loc, scl(d1, kBounceBias));
-            ray_d = normalize(d1);
+            pre.o = add(h.loc, scl(d1, kBounceBias));  // the next ray (state kRayReady)
+            pre.d = normalize(d1);
             state = kRayReady;
             return;
         }
@@ -418,8 +419,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         wo_y = wo_world.y;
         const V3 d1 = normalize(wo_world);
         ++bounces;
-        ray_o = add(h.loc, scl(d1, kBounceBias));
-        ray_d = normalize(d1);
+        pre.o = add(h.loc, scl(d1, kBounceBias));  // the next ray (state kRayReady)
+        pre.d = normalize(d1);
         state = kRayReady;
     };
 
@@ -531,13 +532,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 depth = -1;
                 bounces = 0;
                 flags = 0;
-                ray_o = mk(S.camera[0], S.camera[1], S.camera[2]);
-                ray_d = normalize(mk(x, y, 1.0));
+                pre.o = mk(S.camera[0], S.camera[1], S.camera[2]);
+                pre.d = normalize(mk(x, y, 1.0));
                 state = kRayReady;
             }
             if (state == kRayReady) {
                 VR_SEC(5);
-                begin_ray(ray_o, ray_d);
+                begin_ray();
             }
             VR_STAMP(2);
 
@@ -621,6 +622,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     node = -1;  // this BVH is walked; its pending leaves remain
                 }
             }
+            VR_STAMP(3);
             // leaf round: enough lanes have a pending triangle, or enough lanes (or all) are
             // stalled on theirs
             const uint64_t pm = __ballot(np > 0);
@@ -636,6 +638,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     }
                 }
             }
+            VR_STAMP(4);
             if (state == kTraversing && node < 0 && np == 0) {
                 VR_SEC(8);
                 ++bvh_i;
