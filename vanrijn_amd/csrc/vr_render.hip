@@ -240,8 +240,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     auto finish = [&](double wl, double I) {
         VR_SEC(6);
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
-        out[0] = wl;
-        out[1] = I;
+        // streamed once to HBM and read once by the reduce: non-temporal, so the 16 B per sample
+        // (4.3 GB per 1024^2 x 256 frame) do not evict the BVH and triangles from L2 and MALL
+        __builtin_nontemporal_store(wl, &out[0]);
+        __builtin_nontemporal_store(I, &out[1]);
         if (RECORD) {
             const double Is = I * 360.0;
             const V3 c = xyz_for_wavelength(wl);
@@ -690,8 +692,9 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     }
     for (uint32_t s = 0; s < spp; ++s) {
         const double* ph = staging + ((uint64_t)s * npix + p) * 2;  // final photon {wavelength, intensity}
-        const double Is = ph[1] * 360.0;                            // photon.rs:26-28, camera.rs:121-126
-        const V3 cx = xyz_for_wavelength(ph[0]);                    // colour_xyz.rs:31-35
+        const double wl = __builtin_nontemporal_load(&ph[0]), I = __builtin_nontemporal_load(&ph[1]);
+        const double Is = I * 360.0;                                // photon.rs:26-28, camera.rs:121-126
+        const V3 cx = xyz_for_wavelength(wl);                       // colour_xyz.rs:31-35
         const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
         const double wy = 1.0 - wb;
         const double wt = w + wy;
