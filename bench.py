@@ -38,11 +38,11 @@ METRIC = "Msamples/s + achieved HBM GB/s, 1024x1024 bunny @256spp, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x5EED0001
 
-# algorithmic bytes (DESIGN.md "Roofline"): one f64 AABB per box test, the two child links of a
-# node visit, the 72 B of vertices per triangle test, vertices + normals (144 B) to shade a
-# triangle hit, and the 8-f64 per-pixel accumulation record written once per launch.
+# algorithmic bytes (DESIGN.md "Roofline"): one f64 AABB per box test, the four child links of a
+# (4-wide) node visit, the 72 B of vertices per triangle test, vertices + normals (144 B) to shade
+# a triangle hit, and the 8-f64 per-pixel accumulation record written once per launch.
 BYTES_PER_BOX_TEST = 48
-BYTES_PER_NODE_VISIT = 8
+BYTES_PER_NODE_VISIT = 16
 BYTES_PER_TRI_TEST = 72
 BYTES_PER_SHADED_TRI = 144
 BYTES_PER_PIXEL_STATE = 64
