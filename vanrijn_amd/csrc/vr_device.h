@@ -397,6 +397,24 @@ __device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p
     return distance;
 }
 
+// Conservative f32 pre-test for Sphere::intersect: true only if the LINE passes the sphere so far
+// outside that the reference's f64 discriminant b^2 - 4ac is certainly negative (the call returns
+// None).  In exact arithmetic delta = 4|d|^2 (r^2 - dist^2), dist^2 = |oc|^2 - (oc.d)^2 / |d|^2;
+// the f64 evaluation errs by O(1e-16 (|o|^2 + |c|^2 + |oc|^2)) and this f32 estimate of
+// dist^2 - r^2 by < 2e-6 |oc|^2 (|d| = 1 +- 1e-16; conversions, products and sums each 6e-8
+// relative), so the margin 1e-4 |oc|^2 + 1e-12 (|o|^2 + |c|^2) covers both.  NaN: not missed.
+__device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p) {
+    const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
+    const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
+    const float t = ox * dx + oy * dy + oz * dz;
+    const float oc2 = ox * ox + oy * oy + oz * oz;
+    const float r = (float)s.scalar;
+    const float po = (float)p.o.x * (float)p.o.x + (float)p.o.y * (float)p.o.y + (float)p.o.z * (float)p.o.z;
+    const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
+                     (float)s.vec[2] * (float)s.vec[2];
+    return (oc2 - t * t) - r * r > 1e-4f * oc2 + 1e-12f * (po + pc);
+}
+
 // Plane::intersect (plane.rs:49-75): t or -1 (t == 0 is a hit).  NaN t (ray inside the plane)
 // is reported as a hit with NaN distance, as in the reference; it never wins a comparison here.
 __device__ __forceinline__ bool plane_distance(const Prim& pl, const RayPre& p, double& t) {

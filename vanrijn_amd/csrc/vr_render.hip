@@ -214,8 +214,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const Prim& pr = S.prims[i];
             double dd;
             bool ok;
-            if (pr.kind == 0) ok = plane_distance(pr, pre, dd);
-            else { dd = sphere_distance(pr, pre); ok = dd >= 0.0; }
+            if (pr.kind == 0) {
+                ok = plane_distance(pr, pre, dd);
+            } else {
+                // the f64 test is skipped only when every lane's line clearly misses the sphere
+                // (camera rays of a wave are coherent; so are many bounce rays)
+                if (__ballot(!sphere_missed32(pr, pre)) == 0) continue;
+                dd = sphere_distance(pr, pre);
+                ok = dd >= 0.0;
+            }
             if (ok && (!best.kind || dd < best.d)) {  // min_by keeps the first of equals
                 best.d = dd;
                 best.kind = kPrim;
