@@ -574,6 +574,11 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.film[2] = film_h * (1.0 / fh);
         a.film[3] = film_h * 0.5;
     }
+    {
+        const uint64_t bw = (a.tile_width + 7) / 8, bh = (a.tile_height + 7) / 8;
+        a.rcp_blocks = bw * bh ? 1.0 / (double)(bw * bh) : 0.0;
+        a.rcp_bw = bw ? 1.0 / (double)bw : 0.0;
+    }
     a.queue = s->d_queue;
     a.staging = nullptr;
     return a;
@@ -994,6 +999,9 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
     VR_HIP(hipMemGetInfo(&free_b, &total_b));
     const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + s->staging_bytes) / 2);
     uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (16 * npix)));
+    // the kernel decodes work items with 32-bit block indices: (8x8 blocks) x samples < 2^32
+    if (((tw + 7) / 8) * ((th + 7) / 8) * pass >= (1ull << 32))
+        return fail(VR_ERROR_UNSUPPORTED, "too many pixel blocks x samples in one launch (2^32)");
     const size_t need = (size_t)(16 * npix * pass);
     // previous users of the staging buffer must be done before it is reused or resized
     VR_HIP(hipStreamWaitEvent(st, s->staging_free, 0));

@@ -139,6 +139,9 @@ struct RenderArgs {
     // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
     // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
     double film[4];
+    // work-item decode without integer division: 1 / (8x8 blocks per sample round), 1 / (blocks
+    // per row), as f64 (a 32-bit quotient from one f64 product is off by at most one, then fixed)
+    double rcp_blocks, rcp_bw;
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
     double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
     double* state;                // [tile pixels][8]

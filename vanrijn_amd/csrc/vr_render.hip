@@ -508,10 +508,20 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     if (g >= items) {
                         state = kDone;
                     } else {
-                        const uint32_t chunk_i = (uint32_t)(g / per_chunk);
-                        const uint64_t r = g - (uint64_t)chunk_i * per_chunk;
-                        const uint32_t blk = (uint32_t)(r >> 6), l = (uint32_t)(r & 63);
-                        const uint32_t x = (blk % bw) * 8 + (l & 7), y = (blk / bw) * 8 + (l >> 3);
+                        // g = (chunk_i * blocks + blk) * 64 + l; g >> 6 < 2^32 (the host caps
+                        // a launch's items), quotients by f64 reciprocal, corrected by one
+                        const uint32_t gb = (uint32_t)(g >> 6), l = (uint32_t)(g & 63);
+                        const uint32_t nblk = (uint32_t)(per_chunk >> 6);
+                        uint32_t chunk_i = (uint32_t)((double)gb * A.rcp_blocks);
+                        int32_t rem = (int32_t)(gb - chunk_i * nblk);
+                        if (rem < 0) { --chunk_i; rem += (int32_t)nblk; }
+                        if (rem >= (int32_t)nblk) { ++chunk_i; rem -= (int32_t)nblk; }
+                        const uint32_t blk = (uint32_t)rem;
+                        uint32_t by = (uint32_t)((double)blk * A.rcp_bw);
+                        int32_t bx = (int32_t)(blk - by * bw);
+                        if (bx < 0) { --by; bx += (int32_t)bw; }
+                        if (bx >= (int32_t)bw) { ++by; bx -= (int32_t)bw; }
+                        const uint32_t x = (uint32_t)bx * 8 + (l & 7), y = by * 8 + (l >> 3);
                         if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
                             px = x;
                             py = y;
