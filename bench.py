@@ -38,20 +38,27 @@ METRIC = "Msamples/s + achieved HBM GB/s, 1024x1024 bunny @256spp, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x5EED0001
 
-# algorithmic bytes (DESIGN.md "Roofline"): one f64 AABB per box test, the four child links of a
-# (4-wide) node visit, the 72 B of vertices per triangle test, vertices + normals (144 B) to shade
-# a triangle hit, and the 8-f64 per-pixel accumulation record written once per launch.
+# algorithmic bytes, SURVEY.md 8(d)'s per-unit figure (DESIGN.md "Roofline"): one f64 AABB (48 B)
+# per box test, a triangle's 9 f64 vertices (72 B) per triangle test, its 9 f64 normals (72 B) per
+# shaded triangle hit, one f64 (X, Y, Z, W) record (32 B) per pixel.
 BYTES_PER_BOX_TEST = 48
-BYTES_PER_NODE_VISIT = 16
 BYTES_PER_TRI_TEST = 72
-BYTES_PER_SHADED_TRI = 144
-BYTES_PER_PIXEL_STATE = 64
+BYTES_PER_SHADED_TRI = 72
+BYTES_PER_PIXEL_STATE = 32
 
 
 def algorithmic_bytes(c, pixels):
-    return (BYTES_PER_BOX_TEST * c["box_tests"] + BYTES_PER_NODE_VISIT * c["node_visits"] +
-            BYTES_PER_TRI_TEST * c["triangle_tests"] + BYTES_PER_SHADED_TRI * c["shaded_triangle_hits"] +
-            BYTES_PER_PIXEL_STATE * pixels)
+    return (BYTES_PER_BOX_TEST * c["box_tests"] + BYTES_PER_TRI_TEST * c["triangle_tests"] +
+            BYTES_PER_SHADED_TRI * c["shaded_triangle_hits"] + BYTES_PER_PIXEL_STATE * pixels)
+
+
+def layout_bytes(c, pixels):
+    """What this kernel's own layout reads and writes per launch before any cache: a 128-B Node4
+    line per wide-node visit, a 48-B f64 box per exact fallback, the 80-B vertex record per triangle
+    test, vertex + normal records (160 B) per shaded triangle hit, the 16-B staged photon per sample,
+    the 64-B accumulation record per pixel (reported beside the roofline, not in it)."""
+    return (128 * c["node_visits"] + 48 * c["exact_box_tests"] + 80 * c["triangle_tests"] +
+            160 * c["shaded_triangle_hits"] + 16 * c["samples"] + 64 * pixels)
 
 
 def pmc_traffic(args):
@@ -198,6 +205,8 @@ def main():
                      "kernel": "render_kernel", "kernel_ms": round(avg_kernel_s * 1e3, 3),
                      "reduce_kernel_ms": round(sum(reduce_ms) / len(reduce_ms), 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
+                     "layout_bytes_per_launch": layout_bytes(counts, W * H),
+                     "layout_gbs": round(layout_bytes(counts, W * H) / avg_kernel_s / 1e9, 2),
                      "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests",
                                                                     "rays", "shaded_triangle_hits", "samples",
                                                                     "traversal_slots", "path_loop_slots",
