@@ -353,6 +353,62 @@ struct WideBuilder {
     }
 };
 
+// The 4-wide tree over a device-built (median-split) binary tree, planned on the host from the
+// triangle count alone: that tree's shape depends only on n (a node over n leaves splits n/2 :
+// n - n/2; pre-order indices, the left subtree's m leaves take m - 1 indices), so no node has to
+// come back from the device.  Parity collapse: one wide node per binary node at even depth, its
+// children the binary node's children or, for interior ones, their two children.  desc: per wide
+// node the four slots' box sources (binary node * 2 + child, -1 empty) then their child links;
+// vr_build.hip's fill_wide_kernel gathers the boxes.
+struct ShapeWide {
+    std::vector<int32_t> desc;
+    int stack = 0;
+    int32_t tri_base = 0;
+    struct Sub {
+        uint64_t lo, hi;
+        int32_t idx;  // global binary index when hi - lo >= 2
+    };
+    static void kids(const Sub& p, Sub out[2]) {
+        const uint64_t mid = p.lo + (p.hi - p.lo) / 2;
+        out[0] = {p.lo, mid, p.idx + 1};
+        out[1] = {mid, p.hi, p.idx + (int32_t)(mid - p.lo)};
+    }
+    int32_t wide(const Sub& b, int pushed) {
+        const int32_t me = (int32_t)(desc.size() / 8);
+        desc.resize(desc.size() + 8, -1);
+        int32_t src[4];
+        Sub sub[4];
+        int n = 0;
+        Sub c[2];
+        kids(b, c);
+        for (int i = 0; i < 2; ++i) {
+            if (c[i].hi - c[i].lo == 1) {
+                src[n] = b.idx * 2 + i;
+                sub[n++] = c[i];
+            } else {
+                Sub g[2];
+                kids(c[i], g);
+                for (int j = 0; j < 2; ++j) {
+                    src[n] = c[i].idx * 2 + j;
+                    sub[n++] = g[j];
+                }
+            }
+        }
+        int interior = 0;
+        for (int k = 0; k < n; ++k) interior += sub[k].hi - sub[k].lo > 1;
+        const int here = pushed + std::max(0, interior - 1);
+        stack = std::max(stack, here);
+        for (int k = 0; k < 4; ++k) {
+            int32_t code = vr::kEmptyChild;
+            if (k < n)
+                code = sub[k].hi - sub[k].lo == 1 ? ~(tri_base + (int32_t)sub[k].lo) : wide(sub[k], here);
+            desc[(size_t)me * 8 + k] = k < n ? src[k] : -1;
+            desc[(size_t)me * 8 + 4 + k] = code;
+        }
+        return me;
+    }
+};
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -371,6 +427,7 @@ struct vr_scene {
     std::vector<vr::Node4> nodes4;  // the render kernel's 4-wide tree (collapse_wide)
     std::vector<vr::Node4x> nodes4x;
     int wide_stack = 0;             // deepest traversal stack of the 4-wide tree
+    uint64_t wide_count = 0;        // its node count
     std::vector<vr::TriVerts> tris;
     std::vector<vr::TriNormals> normals;
     std::vector<std::vector<uint64_t>> leaf_order;  // per mesh
@@ -422,6 +479,7 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     WideBuilder W(nodes, s->nodes4, s->nodes4x);
     for (auto& b : s->bvhs) b.root4 = b.root >= 0 ? W.collapse(b.root, 0) : b.root;
     s->wide_stack = W.stack;
+    s->wide_count = s->nodes4.size();
 }
 
 template <class T>
@@ -503,11 +561,32 @@ int upload(vr_scene* s) {
             s->max_depth = std::max(s->max_depth, levels);
         }
         VR_HIP(hipStreamSynchronize(cs.stream));
+        // the 4-wide traversal tree: planned from the meshes' sizes (ShapeWide), boxes gathered on
+        // the device
+        ShapeWide W;
+        for (const auto& pm : s->pending) {
+            if (pm.n < 2) continue;  // one-triangle mesh: its root is the leaf
+            W.tri_base = pm.tri_base;
+            const int32_t root = W.wide({0, pm.n, pm.node_base}, 0);
+            for (auto& b : s->bvhs)
+                if (b.tri_base == pm.tri_base && b.root == pm.node_base) b.root4 = root;
+        }
+        for (auto& b : s->bvhs)
+            if (b.root < 0) b.root4 = b.root;
+        s->wide_stack = W.stack;
+        s->wide_count = W.desc.size() / 8;
+        if (s->wide_count) {
+            int32_t* d_desc = nullptr;
+            VR_HIP(hipMalloc(&d_desc, W.desc.size() * sizeof(int32_t)));
+            const hipError_t ec = hipMemcpy(d_desc, W.desc.data(), W.desc.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+            const int e = ec != hipSuccess ? (int)ec
+                                           : vr::device_fill_wide(nodes, d_desc, s->wide_count, (vr::Node4*)(base + off[7]),
+                                                                  (vr::Node4x*)(base + off[8]), cs.stream);
+            const hipError_t es = hipStreamSynchronize(cs.stream);
+            (void)hipFree(d_desc);
+            if (e || es != hipSuccess) return fail(VR_ERROR_DEVICE, "device wide-tree fill failed");
+        }
         s->pending.clear();  // the caller's arrays are not kept
-        // the 4-wide traversal tree: collapsed on the host from the device-built nodes
-        std::vector<vr::Node> bin(s->node_count);
-        if (sz_nodes) VR_HIP(hipMemcpy(bin.data(), nodes, sz_nodes, hipMemcpyDeviceToHost));
-        collapse_wide(s, bin);
         if (sz_bvh) VR_HIP(hipMemcpy(base + off[5], s->bvhs.data(), sz_bvh, hipMemcpyHostToDevice));
     }
     if (!s->nodes4.empty()) {
@@ -947,7 +1026,7 @@ int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     out->object_count = s->object_count;
     out->extent = s->extent;
     out->device_bytes = s->device_bytes;
-    out->wide_node_count = s->nodes4.size();
+    out->wide_node_count = s->wide_count;
     out->traversal_stack = (uint32_t)s->wide_stack;
     out->reserved = 0;
     return VR_OK;

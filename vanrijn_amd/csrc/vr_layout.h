@@ -187,6 +187,8 @@ int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rg
 int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
                      Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
                      int* levels, void* stream);
+// vr_build.hip: Node4 / Node4x records from a device-built binary tree and a host-made descriptor
+int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, Node4x* out4x, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 
