@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build an A/B variant of the library with extra compile flags into ab/lib<name>.so
+# (the in-tree library is untouched):  bash tools/build_variant.sh NAME -DVR_PEND=12 ...
+set -eu
+cd "$(dirname "$0")/.."
+NAME=$1; shift
+OUT=$(mktemp -d)
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall"
+for s in vr_render.hip vr_image.hip vr_build.hip vr_host.cpp; do
+  /opt/rocm/bin/hipcc $FLAGS "$@" -c vanrijn_amd/csrc/$s -o $OUT/${s%.*}.o &
+done
+wait
+mkdir -p ab
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUT/*.o -lz -o ab/lib$NAME.so
+rm -rf "$OUT"
+echo ab/lib$NAME.so

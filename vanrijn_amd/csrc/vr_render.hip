@@ -15,9 +15,10 @@
 //     end of sample + next camera ray) and a traversal phase that steps BVH nodes for every
 //     traversing lane until 56 lanes wait to shade;
 //   * traversal: per-lane ordered stack walk (LDS stack [depth][thread], node indices only) over
-//     64-B f32 nodes with outward-rounded boxes; a box test too close to call in f32 is re-run
-//     exactly in f64 on the 128-B node; leaf triangles are queued (4 per lane) and tested in f64
-//     in leaf rounds when 2 lanes stall, so the triangle test runs for many lanes at once;
+//     a 4-wide tree of 128-B f32 nodes with outward-rounded boxes; a box test too close to call
+//     in f32 is re-run exactly in f64 on the 192-B Node4x; leaf triangles are queued (8 per lane,
+//     LDS) and tested in f64 in leaf rounds when 2 lanes stall, so the triangle test runs for many
+//     lanes at once;
 //   * each sample's final photon {wavelength, intensity} goes to a staging buffer;
 //     accumulate_kernel turns it into XYZ and folds the samples of a pixel in sample order with
 //     the reference's Kahan update_pixel, so the buffers are bit-identical to sequential calls.
@@ -79,7 +80,10 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
 
 // kRayReady: the lane's next ray (pre.o, pre.d) is set and begin_ray runs once for all such
 // lanes at the end of phase A (one inlined copy for bounce and camera rays alike)
-constexpr int kPend = 8;  // pending leaf triangles per lane (LDS)
+#ifndef VR_PEND
+#define VR_PEND 8
+#endif
+constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
