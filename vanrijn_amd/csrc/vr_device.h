@@ -323,6 +323,20 @@ __device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo
     return 2;
 }
 
+// A triangle record in one batch of five dwordx4 loads.  Left to itself the scheduler issued the
+// last vertex's z only after the first four loads had returned (two memory round trips per
+// triangle test); the empty asm needs all five values at once, so all five are in flight together.
+__device__ __forceinline__ TriVerts load_tri(const TriVerts* p) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4* q = reinterpret_cast<const u4*>(p);
+    u4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3), "+v"(w4));
+    const u4 w[5] = {w0, w1, w2, w3, w4};
+    TriVerts t;
+    __builtin_memcpy(&t, w, sizeof t);
+    return t;
+}
+
 // Triangle::intersect decision part (triangle.rs:35-66): returns distance, or -1 on a miss
 // (a valid hit's distance is a norm, >= 0).  Vertices are translated by -origin (v + (-o) ==
 // v - o bitwise), permuted so the ray's largest signed component is last, sheared (z unscaled).
