@@ -69,6 +69,26 @@ def lib():
             "orc_plane_intersect": (None, [p, p, p, d, p, p, p]),
             "orc_mat3_inverse": (C.c_int, [p, p]),
             "orc_mat3_determinant": (d, [p]),
+            "orc_mat3_first_minor": (d, [p, i32, i32]),
+            "orc_mat3_cofactor_matrix": (None, [p, p]),
+            "orc_mat3_transpose": (None, [p, p]),
+            "orc_mat3_mul": (None, [p, p, p]),
+            "orc_mat3_mul_vec": (None, [p, p, p]),
+            "orc_change_of_basis": (None, [p, p, p, p]),
+            "orc_interval_new": (None, [d, d, p]),
+            "orc_interval_union": (None, [p, p, p]),
+            "orc_interval_intersection": (None, [p, p, p]),
+            "orc_interval_expand": (None, [p, d, p]),
+            "orc_interval_is_empty": (C.c_int, [p]),
+            "orc_interval_is_degenerate": (C.c_int, [p]),
+            "orc_interval_contains": (C.c_int, [p, d]),
+            "orc_bbox_from_corners": (None, [p, p, p]),
+            "orc_bbox_from_points": (None, [i64, p, p]),
+            "orc_bbox_union": (None, [p, p, p]),
+            "orc_bbox_contains_point": (C.c_int, [p, p]),
+            "orc_bbox_largest_dimension": (C.c_int, [p]),
+            "orc_ray_new": (None, [p, p, p, p]),
+            "orc_ray_point_at": (None, [p, p, d, p]),
             "orc_spectrum_intensity": (d, [d, d, i32, p, d]),
             "orc_reflection_from_linear_rgb": (None, [d, d, d, p]),
             "orc_colour_xyz_for_wavelength": (None, [d, p]),
@@ -167,6 +187,114 @@ def mat3_inverse(m):
 
 def mat3_determinant(m):
     return lib().orc_mat3_determinant(_ptr(f64(m, 9)))
+
+
+def mat3_first_minor(m, row, column):
+    return lib().orc_mat3_first_minor(_ptr(f64(m, 9)), row, column)
+
+
+def _mat_out(fn, *args):
+    out = np.zeros(9)
+    fn(*[_ptr(a) for a in args], _ptr(out))
+    return out.reshape(3, 3)
+
+
+def mat3_cofactor_matrix(m):
+    return _mat_out(lib().orc_mat3_cofactor_matrix, f64(m, 9))
+
+
+def mat3_transpose(m):
+    return _mat_out(lib().orc_mat3_transpose, f64(m, 9))
+
+
+def mat3_mul(a, b):
+    return _mat_out(lib().orc_mat3_mul, f64(a, 9), f64(b, 9))
+
+
+def mat3_mul_vec(m, v):
+    out = np.zeros(3)
+    lib().orc_mat3_mul_vec(_ptr(f64(m, 9)), _ptr(f64(v, 3)), _ptr(out))
+    return out
+
+
+def change_of_basis(x, y, z):
+    return _mat_out(lib().orc_change_of_basis, f64(x, 3), f64(y, 3), f64(z, 3))
+
+
+# Interval {min, max} (util/interval.rs) and util BoundingBox {min x, max x, ..., max z}
+def interval_new(a, b):
+    out = np.zeros(2)
+    lib().orc_interval_new(a, b, _ptr(out))
+    return out
+
+
+def interval_union(a, b):
+    out = np.zeros(2)
+    lib().orc_interval_union(_ptr(f64(a, 2)), _ptr(f64(b, 2)), _ptr(out))
+    return out
+
+
+def interval_intersection(a, b):
+    out = np.zeros(2)
+    lib().orc_interval_intersection(_ptr(f64(a, 2)), _ptr(f64(b, 2)), _ptr(out))
+    return out
+
+
+def interval_expand(a, v):
+    out = np.zeros(2)
+    lib().orc_interval_expand(_ptr(f64(a, 2)), v, _ptr(out))
+    return out
+
+
+def interval_is_empty(a):
+    return bool(lib().orc_interval_is_empty(_ptr(f64(a, 2))))
+
+
+def interval_is_degenerate(a):
+    return bool(lib().orc_interval_is_degenerate(_ptr(f64(a, 2))))
+
+
+def interval_contains(a, v):
+    return bool(lib().orc_interval_contains(_ptr(f64(a, 2)), v))
+
+
+def bbox_from_corners(a, b):
+    out = np.zeros(6)
+    lib().orc_bbox_from_corners(_ptr(f64(a, 3)), _ptr(f64(b, 3)), _ptr(out))
+    return out
+
+
+def bbox_from_points(points):
+    p = f64(points).reshape(-1, 3)
+    out = np.zeros(6)
+    lib().orc_bbox_from_points(len(p), _ptr(p), _ptr(out))
+    return out
+
+
+def bbox_union(a, b):
+    out = np.zeros(6)
+    lib().orc_bbox_union(_ptr(f64(a, 6)), _ptr(f64(b, 6)), _ptr(out))
+    return out
+
+
+def bbox_contains_point(b, p):
+    return bool(lib().orc_bbox_contains_point(_ptr(f64(b, 6)), _ptr(f64(p, 3))))
+
+
+def bbox_largest_dimension(b):
+    return lib().orc_bbox_largest_dimension(_ptr(f64(b, 6)))
+
+
+def ray_new(origin, direction):
+    o, d = np.zeros(3), np.zeros(3)
+    lib().orc_ray_new(_ptr(f64(origin, 3)), _ptr(f64(direction, 3)), _ptr(o), _ptr(d))
+    return o, d
+
+
+def ray_point_at(origin, direction, t):
+    out = np.zeros(3)
+    lib().orc_ray_point_at(_ptr(f64(origin, 3)), _ptr(f64(direction, 3)), t, _ptr(out))
+    return out
 
 
 def spectrum_intensity(shortest, longest, samples, wavelength):

@@ -172,6 +172,38 @@ double orc_mat3_determinant(const double in[9]) {
     memcpy(m.e, in, sizeof m.e);
     return determinant(&m);
 }
+/* mat3.rs:72-90 (first_minor), :96-104 (cofactor_matrix), :62-70 (transpose), :121-132 (Mat3 *
+ * Mat3: row(i) . column(j)), :147-157 (Mat3 * Vec3); exported for the reference's mat3 tests */
+double orc_mat3_first_minor(const double in[9], int32_t row, int32_t column) {
+    m3 m;
+    memcpy(m.e, in, sizeof m.e);
+    return first_minor(&m, row, column);
+}
+void orc_mat3_cofactor_matrix(const double in[9], double out[9]) {
+    m3 m;
+    memcpy(m.e, in, sizeof m.e);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out[3 * i + j] = cofactor(&m, i, j);
+}
+void orc_mat3_transpose(const double in[9], double out[9]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out[3 * i + j] = in[3 * j + i];
+}
+void orc_mat3_mul(const double a[9], const double b[9], double out[9]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            out[3 * i + j] = dot(mk(a[3 * i], a[3 * i + 1], a[3 * i + 2]), mk(b[j], b[3 + j], b[6 + j]));
+}
+void orc_mat3_mul_vec(const double in[9], const double v[3], double out[3]) {
+    m3 m;
+    memcpy(m.e, in, sizeof m.e);
+    st(out, mul_mv(&m, ld(v)));
+}
+/* util/algebra_utils.rs:3-5: try_change_of_basis_matrix = Some(Mat3::from_rows(x, y, z)) */
+void orc_change_of_basis(const double x[3], const double y[3], const double z[3], double out[9]) {
+    m3 m = from_rows(ld(x), ld(y), ld(z));
+    memcpy(out, m.e, sizeof m.e);
+}
 
 /* ======================================================================================== */
 /* Interval / BoundingBox (src/util/interval.rs, src/util/axis_aligned_bounding_box.rs)     */
@@ -248,6 +280,50 @@ int orc_bbox_intersect(const double bmin[3], const double bmax[3], const double 
     return slab(&bb, ld(o), ld(d), &a, &b);
 }
 
+/* Interval (util/interval.rs:7-87) and util BoundingBox (util/axis_aligned_bounding_box.rs:11-99)
+ * exported as {min, max} pairs / six doubles {min x, max x, min y, max y, min z, max z}, for the
+ * reference's interval and bbox tests.  contains_value: interval.rs:53-55. */
+static ival ival_ld(const double a[2]) { ival r = {a[0], a[1]}; return r; }
+static void ival_st(double out[2], ival a) { out[0] = a.min; out[1] = a.max; }
+void orc_interval_new(double a, double b, double out[2]) { ival_st(out, ival_new(a, b)); }
+void orc_interval_union(const double a[2], const double b[2], double out[2]) {
+    ival_st(out, ival_union(ival_ld(a), ival_ld(b)));
+}
+void orc_interval_intersection(const double a[2], const double b[2], double out[2]) { /* interval.rs:57-62 */
+    ival r = {fmax(a[0], b[0]), fmin(a[1], b[1])};
+    ival_st(out, r);
+}
+void orc_interval_expand(const double a[2], double v, double out[2]) { ival_st(out, ival_expand(ival_ld(a), v)); }
+int orc_interval_is_empty(const double a[2]) { return ival_is_empty(ival_ld(a)); }
+int orc_interval_is_degenerate(const double a[2]) { return ival_is_degenerate(ival_ld(a)); }
+int orc_interval_contains(const double a[2], double v) { return v >= a[0] && v <= a[1]; }
+
+static bbox bbox_ld(const double b[6]) {
+    bbox r;
+    for (int i = 0; i < 3; ++i) { r.b[i].min = b[2 * i]; r.b[i].max = b[2 * i + 1]; }
+    return r;
+}
+static void bbox_st(double out[6], bbox b) {
+    for (int i = 0; i < 3; ++i) { out[2 * i] = b.b[i].min; out[2 * i + 1] = b.b[i].max; }
+}
+void orc_bbox_from_corners(const double a[3], const double b[3], double out[6]) { /* :11-21 */
+    bbox r;
+    for (int i = 0; i < 3; ++i) r.b[i] = ival_new(a[i], b[i]);
+    bbox_st(out, r);
+}
+void orc_bbox_from_points(int64_t n, const double* pts, double out[6]) { /* :40-47 fold expand_to_point */
+    bbox r = bbox_empty();
+    for (int64_t k = 0; k < n; ++k) r = bbox_expand(r, ld(pts + 3 * k));
+    bbox_st(out, r);
+}
+void orc_bbox_union(const double a[6], const double b[6], double out[6]) { bbox_st(out, bbox_union(bbox_ld(a), bbox_ld(b))); }
+int orc_bbox_contains_point(const double b[6], const double p[3]) { /* :59-64 */
+    for (int i = 0; i < 3; ++i)
+        if (!(p[i] >= b[2 * i] && p[i] <= b[2 * i + 1])) return 0;
+    return 1;
+}
+int orc_bbox_largest_dimension(const double b[6]) { return largest_dimension(bbox_ld(b)); }
+
 /* ======================================================================================== */
 /* Ray (src/raycasting/mod.rs:29-61)                                                        */
 /* ======================================================================================== */
@@ -257,6 +333,16 @@ typedef struct ray {
 static ray ray_new(v3 o, v3 d) { ray r = {o, normalize(d)}; return r; }
 static v3 point_at(const ray* r, double t) { return add(r->o, scl(r->d, t)); }
 static ray ray_bias(const ray* r, double a) { return ray_new(point_at(r, a), r->d); }
+/* Ray::new / point_at (mod.rs:41-52), exported for the reference's ray tests (mod.rs:155-181) */
+void orc_ray_new(const double o[3], const double d[3], double out_o[3], double out_d[3]) {
+    ray r = ray_new(ld(o), ld(d));
+    st(out_o, r.o);
+    st(out_d, r.d);
+}
+void orc_ray_point_at(const double o[3], const double d[3], double t, double out[3]) {
+    ray r = {ld(o), ld(d)};
+    st(out, point_at(&r, t));
+}
 
 /* ======================================================================================== */
 /* Primitives                                                                               */

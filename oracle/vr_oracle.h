@@ -12,7 +12,10 @@
  *     (src/raycasting/sphere.rs:112-184), plane (src/raycasting/plane.rs:118-297),
  *     spectrum lookup (src/colour/spectrum.rs:427-488), CIE round trip
  *     (src/colour/colour_xyz.rs:127-133), accumulation buffer (src/accumulation_buffer.rs:127-327),
- *     Mat3 (src/math/mat3.rs:185-357), camera (src/camera.rs:143-182).
+ *     Mat3 (src/math/mat3.rs:185-357), camera (src/camera.rs:143-182), Ray
+ *     (src/raycasting/mod.rs:155-181), change of basis (src/util/algebra_utils.rs:16-49),
+ *     Interval (src/util/interval.rs:97-327), util BoundingBox
+ *     (src/util/axis_aligned_bounding_box.rs:108-239).
  *   - UNPINNED (the reference has no tests for them and cannot be built here: no Rust
  *     toolchain): BVH traversal, sampler, integrator, materials,
  *     reflection_from_linear_rgb, CMF values, whole images.  Restated line by line instead.
@@ -64,6 +67,27 @@ void orc_plane_intersect(const double n[3], const double t[3], const double c[3]
                          const double d[3], orc_hit* out);
 int orc_mat3_inverse(const double m[9], double out[9]); /* cofactor^T * det, as mat3.rs:111-118 */
 double orc_mat3_determinant(const double m[9]);
+double orc_mat3_first_minor(const double m[9], int32_t row, int32_t column);
+void orc_mat3_cofactor_matrix(const double m[9], double out[9]);
+void orc_mat3_transpose(const double m[9], double out[9]);
+void orc_mat3_mul(const double a[9], const double b[9], double out[9]);
+void orc_mat3_mul_vec(const double m[9], const double v[3], double out[3]);
+void orc_change_of_basis(const double x[3], const double y[3], const double z[3], double out[9]);
+/* Interval as {min, max}; util BoundingBox as {min x, max x, min y, max y, min z, max z} */
+void orc_interval_new(double a, double b, double out[2]);
+void orc_interval_union(const double a[2], const double b[2], double out[2]);
+void orc_interval_intersection(const double a[2], const double b[2], double out[2]);
+void orc_interval_expand(const double a[2], double v, double out[2]);
+int orc_interval_is_empty(const double a[2]);
+int orc_interval_is_degenerate(const double a[2]);
+int orc_interval_contains(const double a[2], double v);
+void orc_bbox_from_corners(const double a[3], const double b[3], double out[6]);
+void orc_bbox_from_points(int64_t n, const double* pts, double out[6]);
+void orc_bbox_union(const double a[6], const double b[6], double out[6]);
+int orc_bbox_contains_point(const double b[6], const double p[3]);
+int orc_bbox_largest_dimension(const double b[6]);
+void orc_ray_new(const double o[3], const double d[3], double out_o[3], double out_d[3]);
+void orc_ray_point_at(const double o[3], const double d[3], double t, double out[3]);
 double orc_spectrum_intensity(double shortest, double longest, int32_t n, const double* samples, double wavelength);
 void orc_reflection_from_linear_rgb(double r, double g, double b, double out[32]);
 void orc_colour_xyz_for_wavelength(double wavelength, double out[3]);
