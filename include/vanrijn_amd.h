@@ -15,7 +15,14 @@
  *     calling thread is in vr_last_error().  Nothing unwinds across the ABI; where the reference
  *     panics (singular shading basis, out-of-range tile) the call returns an error instead.
  *   - A vr_scene is immutable after creation and may be shared by any number of threads;
- *     render calls are re-entrant (each call uses its own stream and scratch).
+ *     render calls are re-entrant.  Each call holds its own stream, staging buffer, work-queue
+ *     counter and device error word for its duration (a per-scene pool of call contexts), so
+ *     concurrent calls neither serialise on shared scratch nor see each other's errors
+ *     (tests/test_gpu_concurrency.py).
+ *   - Errors found on the device (the singular shading basis where the reference panics,
+ *     simple_random_integrator.rs:26-31) belong to the call that found them: synchronous entry
+ *     points return them; the asynchronous vr_render_tile_device records them in a sticky word of
+ *     its stream, returned by the next vr_stream_check_error (or timed launch) on that stream.
  */
 #ifndef VANRIJN_AMD_H
 #define VANRIJN_AMD_H
@@ -27,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 3
+#define VR_ABI_VERSION 4
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -212,8 +219,8 @@ typedef struct vr_render_params {
 
 /* Replaces partial_render_scene (camera.rs:95-130) one-for-one: one sample per pixel into a
  * fresh tile buffer (`out` arrays are caller-allocated host memory, tile-sized).  The sample
- * index comes from a per-scene atomic pass counter, so concurrent callers get distinct random
- * streams like the reference's thread_rng.  Thread-safe. */
+ * index comes from a per-scene atomic pass counter starting at 0 (seed 0x5EED0001), so concurrent
+ * callers get distinct random streams like the reference's thread_rng.  Thread-safe. */
 int vr_partial_render_scene(const vr_scene* scene, vr_tile tile, uint64_t height, uint64_t width,
                             vr_accumulation_buffer* out);
 
@@ -246,11 +253,20 @@ typedef struct vr_launch_stats {
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
+/* Waits for `stream` and returns the first device error (VR_ERROR_SINGULAR_BASIS) of any
+ * vr_render_tile_device launch of `scene` on that stream since the last check, then clears it
+ * (ABI 4).  A VR_LAUNCH_TIMED launch performs this check itself. */
+int vr_stream_check_error(const vr_scene* scene, void* stream);
 /* Mean XYZ of host-side state records: colour = colour_sum * (1 / weight)
  * (accumulation_buffer.rs:59).  States of disjoint sample sets (e.g. one per GPU) merge by
  * element-wise addition of the 8-double records (the cross-GPU reduce), which is what
  * AccumulationBuffer::merge_tile's weighted blend (accumulation_buffer.rs:62-85) computes. */
 int vr_resolve_state(const double* state_host, uint64_t pixel_count, double* colour_out);
+/* AccumulationBuffer::merge_tile (accumulation_buffer.rs:62-85, the host side of main.rs:214-216):
+ * for every pixel of `tile` (full-image coordinates in `dst`), dst colour = blend(dst colour, dst
+ * weight, src colour, src weight) = (c1 * w1 + c2 * w2) * (1 / (w1 + w2)); dst weight += src
+ * weight.  dst's colour_sum / bias buffers are not touched (as in the reference).  Host only (ABI 4). */
+int vr_merge_tile(vr_accumulation_buffer* dst, vr_tile tile, const vr_accumulation_buffer* src);
 
 /* Per-(pixel, sample) records, for decision-identity checks against the oracle. */
 typedef struct vr_sample_record {

@@ -40,7 +40,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 3
+    assert lib.vr_abi_version() == 4
     assert isinstance(lib.vr_last_error(), bytes)
 
 
@@ -83,3 +83,28 @@ def test_load_obj_missing_file_is_io_error(tmp_path):
         assert e.code == -6
     else:
         raise AssertionError
+
+
+def test_merge_tile_matches_oracle(oracle):
+    """vr_merge_tile (host code in the library) == the oracle's merge_tile (accumulation_buffer.rs:62-85)."""
+    from vanrijn_amd.render import AccumulationBuffer, Tile
+    g = np.random.default_rng(5)
+    W, H = 13, 9
+    dst = AccumulationBuffer(W, H)
+    dst.colour_buffer[...] = g.uniform(0, 2, (H, W, 3))
+    dst.weight_buffer[...] = g.integers(1, 9, (H, W)).astype(float)
+    t = Tile(3, 10, 2, 7)
+    src = AccumulationBuffer(t.width(), t.height())
+    src.colour_buffer[...] = g.uniform(0, 2, (t.height(), t.width(), 3))
+    src.weight_buffer[...] = g.integers(1, 9, (t.height(), t.width())).astype(float)
+    ref_c, ref_w = dst.colour_buffer.copy(), dst.weight_buffer.copy()
+    oracle.lib().orc_merge_tile(W, ref_c.ctypes.data, ref_w.ctypes.data, t.start_row, t.start_column, t.height(),
+                                t.width(), src.colour_buffer.ctypes.data, src.weight_buffer.ctypes.data)
+    dst.merge_tile(t, src)
+    assert np.array_equal(dst.colour_buffer, ref_c) and np.array_equal(dst.weight_buffer, ref_w)
+    try:
+        dst.merge_tile(Tile(0, 3, 0, 3), src)  # size mismatch: the reference asserts (accumulation_buffer.rs:63-64)
+    except N.VrError as e:
+        assert e.code == -1
+    else:
+        raise AssertionError("mismatched merge_tile must fail")

@@ -1,6 +1,13 @@
-"""World-size-2 run of the multi-GPU sharding + reduce on CPU (gloo), with the oracle standing in
-for the GPU renderer of each shard.  Checks the reduced image against one process rendering the
-union of the sample sets."""
+"""World-size 2 and 4 runs of the multi-GPU step on CPU (gloo), with the oracle standing in for the
+GPU renderer of each shard.
+
+Every rank runs vanrijn_amd.distributed.frame_step -- the same function bench.py's step() calls
+with the HIP renderer and RCCL -- for both layouts bench.py has: weak scaling (every rank renders
+`spp` samples per pixel, c1-c3) and one frame's spp split over the ranks (c4 / c5).  The reduced
+records on rank 0 must hold exactly the union's sample counts, its mean within 1e-12 of one
+process rendering the union, and zeroed Kahan compensations (an update_pixel continuation then
+starts a fresh compensated sum, accumulation_buffer.rs:44-60).
+"""
 import os
 import socket
 
@@ -11,6 +18,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from vanrijn_amd import distributed as D
+
+H, W, SEED = 20, 24, 17
 
 
 def _free_port():
@@ -30,38 +39,63 @@ def _records(buf):
                            buf["weight_bias"][..., None]], axis=-1)
 
 
-def _worker(rank, world, port, spp, out_path):
+def _worker(rank, world, port, total_spp, split, steps, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle_ffi as O
     from vanrijn_amd.render import Tile
     orc = O.OracleScene(_small_scene().spec())
-    tile = Tile(0, 24, 0, 20)
+    spp = D.shard_spp(total_spp, world, split)
+    state = torch.zeros(H * W * 8, dtype=torch.float64)
 
-    def shard(first):
-        buf = orc.render_tile(tile, 20, 24, spp, seed=17, first_sample=first, mode=O.MODE_PRUNED)
-        return torch.from_numpy(_records(buf).copy())
+    def shard(first, st):  # the oracle in place of render_tile_device (fresh records per frame)
+        buf = orc.render_tile(Tile(0, W, 0, H), H, W, spp, seed=SEED, first_sample=first, mode=O.MODE_PRUNED)
+        st.copy_(torch.from_numpy(_records(buf).reshape(-1)))
+        return first
 
-    state = D.render_frame(shard, step=0, spp=spp)
+    firsts = [D.frame_step(shard, state, step, spp) for step in range(steps)]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, firsts)
     if rank == 0:
-        np.save(out_path, state.numpy())
+        np.save(out_path, state.numpy().reshape(H, W, 8))
+        np.save(out_path + ".firsts.npy", np.array(gathered))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_frame_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world,split", [(2, False), (4, False), (2, True), (4, True)])
+def test_sharded_frame_matches_single_process(tmp_path, world, split):
     from oracle import oracle_ffi as O
     from vanrijn_amd.render import Tile
-    spp, world = 3, 2
+    total_spp, steps = 4, 2
+    spp = D.shard_spp(total_spp, world, split)
     out = str(tmp_path / "rank0.npy")
-    mp.spawn(_worker, args=(world, _free_port(), spp, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), total_spp, split, steps, out), nprocs=world, join=True)
     reduced = np.load(out)
+    firsts = np.load(out + ".firsts.npy")
+    # the last frame's shards are disjoint and contiguous: [(step*N + r)*spp, +spp)
+    last = sorted(int(f[-1]) for f in firsts)
+    assert last == [((steps - 1) * world + r) * spp for r in range(world)]
+    union_first, union_spp = last[0], world * spp
     orc = O.OracleScene(_small_scene().spec())
-    single = _records(orc.render_tile(Tile(0, 24, 0, 20), 20, 24, world * spp, seed=17, mode=O.MODE_PRUNED))
+    single = _records(orc.render_tile(Tile(0, W, 0, H), H, W, union_spp, seed=SEED, first_sample=union_first,
+                                      mode=O.MODE_PRUNED))
     assert np.array_equal(reduced[..., 6], single[..., 6])  # weights: exact sample counts
+    assert (reduced[..., 3:6] == 0).all() and (reduced[..., 7] == 0).all()  # compensations zeroed on rank 0
     mean_r = D.mean_colour(torch.from_numpy(reduced)).numpy()
     mean_s = D.mean_colour(torch.from_numpy(single)).numpy()
     assert np.abs(mean_r - mean_s).max() < 1e-12
+    # an update_pixel continuation on the reduced state == the same continuation of the union
+    buf = {"colour": np.zeros((H, W, 3)), "colour_sum": reduced[..., 0:3].copy(),
+           "colour_bias": reduced[..., 3:6].copy(), "weight": reduced[..., 6].copy(),
+           "weight_bias": reduced[..., 7].copy()}
+    nxt = union_first + union_spp
+    cont = orc.render_tile(Tile(0, W, 0, H), H, W, 2, seed=SEED, first_sample=nxt, mode=O.MODE_PRUNED,
+                           accumulate=buf)
+    both = orc.render_tile(Tile(0, W, 0, H), H, W, union_spp + 2, seed=SEED, first_sample=union_first,
+                           mode=O.MODE_PRUNED)
+    assert np.array_equal(cont["weight"], both["weight"])
+    assert np.abs(cont["colour"] - both["colour"]).max() < 1e-12
 
 
 def test_first_sample_partition():
@@ -73,3 +107,15 @@ def test_first_sample_partition():
             assert not (block & seen)
             seen |= block
     assert seen == set(range(3 * 4 * 8))
+
+
+def test_shard_spp():
+    assert D.shard_spp(256, 8, False) == 256
+    assert D.shard_spp(1024, 8, True) == 128 and D.shard_spp(256, 8, True) == 32
+    with pytest.raises(ValueError):
+        D.shard_spp(256, 3, True)
+
+
+def test_reduce_is_a_no_op_on_one_process():
+    s = torch.arange(16, dtype=torch.float64)
+    assert torch.equal(D.reduce_records(s.clone()), s)  # no process group: nothing reduced or zeroed

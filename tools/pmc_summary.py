@@ -1,8 +1,14 @@
-"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) for the render kernel into
-profiles/<round>/pmc_summary.json and profiles/pmc_traffic.json (read by bench.py).
+"""Fold rocprofv3 --pmc passes (tools/pmc.sh) of the render kernel into a PMC record.
 
-HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KB units from rocprofv3; FETCH_SIZE doubled
-per the gfx950 caveat in MI355X_MICROARCH.md "HBM": it tallies 128-B requests at 64 B).
+    python tools/pmc_summary.py gpurun_out/pmc/<name> profiles/<round>/pmc_<name>.json
+
+Writes the full summary to the second path and adds / replaces the record of this library build
+and bench config in profiles/pmc_records.json, which bench.py reads for its roofline:
+  per_launch  every counter of the timed render_kernel dispatch (COUNT=false), summed over the
+              rows rocprofv3 writes for it;
+  kernel_ns   that dispatch's duration in the tcc pass (GRBM_GUI_ACTIVE / 8 / kernel_ns = clock);
+HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KB units; FETCH_SIZE doubled per the gfx950
+caveat in MI355X_MICROARCH.md: it tallies 128-B requests at 64 B).
 """
 import collections
 import csv
@@ -15,56 +21,71 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def load(pass_dir, kernel_substr):
+def is_timed_render(name):
+    # render_kernel<STACK, COUNT, RECORD, ...>: the timed launches have COUNT = false
+    if "render_kernel<" not in name:
+        return False
+    targs = name.split("render_kernel<")[1].split(">")[0].split(",")
+    return targs[1].strip() == "false" and targs[2].strip() == "false"
+
+
+def load(pass_dir):
     rows = list(csv.DictReader(open(os.path.join(pass_dir, "run_counter_collection.csv"))))
-    per_dispatch = collections.defaultdict(dict)
+    per = collections.defaultdict(dict)
     for r in rows:
-        if kernel_substr in r["Kernel_Name"] and "true" not in r["Kernel_Name"].split("render_kernel<")[-1][:20]:
-            per_dispatch[int(r["Dispatch_Id"])].setdefault(r["Counter_Name"], 0.0)
-            per_dispatch[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-    return per_dispatch
+        if is_timed_render(r["Kernel_Name"]):
+            d = per[int(r["Dispatch_Id"])]
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    durations = {}
+    trace = os.path.join(pass_dir, "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        for r in csv.DictReader(open(trace)):
+            if is_timed_render(r["Kernel_Name"]):
+                durations[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return per, durations
+
+
+def bench_key(pmc_dir):
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "*.out"))):
+        for line in open(f):
+            line = line.strip()
+            if line.startswith("{"):
+                return json.loads(line)["config"]["pmc_key"]
+    raise SystemExit("no bench JSON line in the pass outputs")
 
 
 def main():
-    pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
-    out_dir = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "r01")
-    args = open(os.path.join(pmc, "args.txt")).read().strip() if os.path.exists(os.path.join(pmc, "args.txt")) else ""
-    summary = {"bench_args": args, "kernel": "vr::dev::render_kernel<.., COUNT=false, ..>", "passes": {}}
-    for d in sorted(glob.glob(os.path.join(pmc, "*/"))):
+    pmc_dir, out_path = sys.argv[1], sys.argv[2]
+    per_launch, kernel_ns = {}, {}
+    for d in sorted(glob.glob(os.path.join(pmc_dir, "*/"))):
         name = os.path.basename(d.rstrip("/"))
-        try:
-            disp = load(d, "render_kernel")
-        except FileNotFoundError:
+        if not os.path.exists(os.path.join(d, "run_counter_collection.csv")):
             continue
+        disp, dur = load(d)
         if not disp:
             continue
-        last = disp[max(disp)]  # the timed step's dispatch (after the counting launch)
-        summary["passes"][name] = last
-    f = summary["passes"].get("fetch", {}).get("FETCH_SIZE")
-    w = summary["passes"].get("write", {}).get("WRITE_SIZE")
+        last = max(disp)  # the timed step's dispatch (after the counting launch)
+        per_launch.update(disp[last])
+        if last in dur:
+            kernel_ns[name] = dur[last]
     lib = os.path.join(ROOT, "vanrijn_amd", "lib", "libvanrijn_amd.so")
     sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
-    if f is not None and w is not None:
-        summary["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
-        summary["fetch_size_kb"] = f
-        summary["write_size_kb"] = w
-    tcc = summary["passes"].get("tcc", {})
-    if tcc.get("TCC_HIT_sum"):
-        summary["l2_hit_rate"] = tcc["TCC_HIT_sum"] / (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"])
-    summary["lib_sha256"] = sha
-    os.makedirs(out_dir, exist_ok=True)
-    json.dump(summary, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
-    if "hbm_bytes_per_launch" in summary:
-        cfg = {"width": 1024, "height": 1024, "spp": 256, "scene": "main"}
-        toks = args.split()
-        for k in cfg:
-            if f"--{k}" in toks:
-                cfg[k] = toks[toks.index(f"--{k}") + 1]
-        config = f"--width {cfg['width']} --height {cfg['height']} --spp {cfg['spp']} --scene {cfg['scene']}"
-        json.dump({"lib_sha256": sha, "config": config, "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
-                   "source": os.path.relpath(os.path.join(out_dir, "pmc_summary.json"), ROOT)},
-                  open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(summary, indent=1))
+    key = bench_key(pmc_dir)
+    rec = {"lib_sha256": sha, "config": key, "per_launch": per_launch,
+           "kernel_ns": kernel_ns.get("tcc") or max(kernel_ns.values()),
+           "kernel_ns_per_pass": kernel_ns, "bench_args": open(os.path.join(pmc_dir, "args.txt")).read().strip(),
+           "source": os.path.relpath(out_path, ROOT)}
+    rec["hbm_bytes_per_launch"] = 2 * per_launch["FETCH_SIZE"] * 1024 + per_launch["WRITE_SIZE"] * 1024
+    os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    json.dump(rec, open(out_path, "w"), indent=1)
+    recs_path = os.path.join(ROOT, "profiles", "pmc_records.json")
+    try:
+        recs = json.load(open(recs_path))
+    except (OSError, ValueError):
+        recs = {}
+    recs[key] = rec
+    json.dump(recs, open(recs_path, "w"), indent=1, sort_keys=True)
+    print(json.dumps({k: rec[k] for k in ("config", "kernel_ns", "hbm_bytes_per_launch", "lib_sha256")}))
 
 
 if __name__ == "__main__":

@@ -133,7 +133,9 @@ SIGNATURES = {
     "vr_partial_render_scene": (C.c_int, [_p, TileC, _u64, _u64, C.POINTER(AccumulationBufferC)]),
     "vr_render_tile": (C.c_int, [_p, C.POINTER(RenderParams), C.POINTER(AccumulationBufferC)]),
     "vr_render_tile_device": (C.c_int, [_p, C.POINTER(RenderParams), _p, _p, _u32, C.POINTER(LaunchStats)]),
+    "vr_stream_check_error": (C.c_int, [_p, _p]),
     "vr_resolve_state": (C.c_int, [_p, _u64, _p]),
+    "vr_merge_tile": (C.c_int, [C.POINTER(AccumulationBufferC), TileC, C.POINTER(AccumulationBufferC)]),
     "vr_render_samples": (C.c_int, [_p, C.POINTER(RenderParams), _p]),
     "vr_trace_rays": (C.c_int, [_p, _u64, _p, _p, _p]),
     "vr_spectrum_reflection_from_linear_rgb": (C.c_int, [_d, _d, _d, _p]),

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/vanrijn_amd.h"
@@ -452,19 +453,36 @@ struct vr_scene {
     void* d_block = nullptr;
     size_t device_bytes = 0;
     vr::DeviceScene dev{};
-    int32_t* d_error = nullptr;
     unsigned long long* d_counters = nullptr;
     std::mutex counter_mutex;
     std::atomic<uint64_t> pass_counter{0};
-    // per-sample staging buffer + work-queue counter, reused across calls; `staging_free` is
-    // recorded after the last kernel that reads them, and every new call's stream waits on it
-    std::mutex staging_mutex;
-    void* staging = nullptr;
-    size_t staging_bytes = 0;
-    unsigned long long* d_queue = nullptr;
-    hipEvent_t staging_free = nullptr;
+    // render-call contexts (stream, staging buffer, work-queue counter, error word, scratch),
+    // pooled: concurrent calls each hold their own, so they neither share a staging buffer nor
+    // read each other's error word (include/vanrijn_amd.h "Threading")
+    std::mutex ctx_mutex;
+    std::vector<struct CallCtx*> ctx_all, ctx_free;
+    // sticky per-stream error words of the asynchronous entry point (vr_render_tile_device),
+    // read and cleared by vr_stream_check_error or a timed launch on that stream
+    std::mutex slot_mutex;
+    std::unordered_map<void*, int32_t*> stream_slots;
     int cu_count = 0;
     uint64_t partial_seed = 0x5EED0001ull;
+    // test hook (VR_FAULT_SINGULAR_OBJECT at scene creation): hits on this object take the
+    // singular-basis path, which finite geometry cannot reach (DESIGN.md "Errors")
+    int32_t fault_object = -1;
+};
+
+// One render call's device resources.  `done` is recorded on the launch stream after the last
+// kernel that reads `staging` / `queue`; a later user of the context waits on it first.
+struct CallCtx {
+    hipStream_t stream = nullptr;  // the host-buffer entry points' own stream
+    hipEvent_t done = nullptr;
+    void* staging = nullptr;  // 16 B per (pixel, sample) of a pass
+    size_t staging_bytes = 0;
+    unsigned long long* queue = nullptr;  // work-item counter; error word at queue + 8
+    int32_t* error = nullptr;
+    void* scratch = nullptr;  // device records + host-layout buffers of the host-buffer calls
+    size_t scratch_bytes = 0;
 };
 
 namespace {
@@ -519,8 +537,6 @@ int upload(vr_scene* s) {
     VR_HIP(hipMalloc(&s->d_block, total));
     s->device_bytes = total;
     VR_HIP(hipDeviceGetAttribute(&s->cu_count, hipDeviceAttributeMultiprocessorCount, s->device));
-    VR_HIP(hipMalloc(&s->d_queue, 256));
-    VR_HIP(hipEventCreateWithFlags(&s->staging_free, hipEventDisableTiming));
     char* base = (char*)s->d_block;
     const void* src[6] = {s->nodes.data(), s->tris.data(), s->normals.data(), s->materials.data(), s->prims.data(),
                           s->bvhs.data()};
@@ -529,7 +545,6 @@ int upload(vr_scene* s) {
         if (sizes[i]) VR_HIP(hipMemcpy(base + off[i], src[i], sizes[i], hipMemcpyHostToDevice));
     }
     VR_HIP(hipMemset(base + off[6], 0, sizes[6]));
-    s->d_error = (int32_t*)(base + off[6]);
     s->d_counters = (unsigned long long*)(base + off[6] + 64);
     s->dev.light_dirs = (const double*)(base + off[6] + sz_misc);
     if (!s->light_dirs.empty())
@@ -627,7 +642,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.records = nullptr;
     a.counters = nullptr;
     a.wg_times = nullptr;
-    a.error_flag = s->d_error;
+    a.error_flag = nullptr;  // per call (enqueue_passes)
+    a.fault_object = s->fault_object;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 56u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
@@ -640,7 +656,6 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 64u;
     const char* ls = getenv("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 2u;
-    a.pad4 = 0;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {
@@ -658,17 +673,18 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.rcp_blocks = bw * bh ? 1.0 / (double)(bw * bh) : 0.0;
         a.rcp_bw = bw ? 1.0 / (double)bw : 0.0;
     }
-    a.queue = s->d_queue;
+    a.queue = nullptr;  // per call (enqueue_passes)
     a.staging = nullptr;
     return a;
 }
 
-int read_and_clear_error(const vr_scene* s, hipStream_t stream) {
+// Waits for `stream`, then reads and clears one error word (a call's own, or a stream's sticky one).
+int read_and_clear_error(int32_t* slot, hipStream_t stream) {
     int32_t flag = 0;
-    VR_HIP(hipMemcpyAsync(&flag, s->d_error, sizeof flag, hipMemcpyDeviceToHost, stream));
+    VR_HIP(hipMemcpyAsync(&flag, slot, sizeof flag, hipMemcpyDeviceToHost, stream));
     VR_HIP(hipStreamSynchronize(stream));
     if (flag) {
-        VR_HIP(hipMemsetAsync(s->d_error, 0, sizeof flag, stream));
+        VR_HIP(hipMemsetAsync(slot, 0, sizeof flag, stream));
         VR_HIP(hipStreamSynchronize(stream));
         return fail(VR_ERROR_SINGULAR_BASIS,
                     "Normal, tangent and cotangent don't form a valid basis (det == 0); the reference panics here");
@@ -676,7 +692,93 @@ int read_and_clear_error(const vr_scene* s, hipStream_t stream) {
     return VR_OK;
 }
 
-// RAII device buffer + stream for the synchronous host-buffer entry points
+// Grow a context buffer to `need` bytes; its previous contents may still be in use by the
+// context's last call (on whatever stream), so wait for `done` before freeing it.
+int ctx_grow(void** ptr, size_t* have, size_t need, hipEvent_t done) {
+    if (need <= *have) return VR_OK;
+    VR_HIP(hipEventSynchronize(done));
+    if (*ptr) VR_HIP(hipFree(*ptr));
+    *ptr = nullptr;
+    *have = 0;
+    VR_HIP(hipMalloc(ptr, need));
+    *have = need;
+    return VR_OK;
+}
+
+void ctx_free_all(CallCtx* c) {
+    if (c->done) {
+        (void)hipEventSynchronize(c->done);
+        (void)hipEventDestroy(c->done);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->staging) (void)hipFree(c->staging);
+    if (c->scratch) (void)hipFree(c->scratch);
+    if (c->queue) (void)hipFree(c->queue);
+    delete c;
+}
+
+// Take a context from the scene's pool (a new one when all are in use).  The caller must hand it
+// back with ctx_release; work it enqueued may still run (its `done` event orders the next user).
+int ctx_acquire(vr_scene* s, CallCtx** out) {
+    {
+        std::lock_guard<std::mutex> g(s->ctx_mutex);
+        if (!s->ctx_free.empty()) {
+            *out = s->ctx_free.back();
+            s->ctx_free.pop_back();
+            return VR_OK;
+        }
+    }
+    CallCtx* c = new (std::nothrow) CallCtx();
+    if (!c) return fail(VR_ERROR_OUT_OF_MEMORY, "call context allocation failed");
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc(&c->queue, 256);
+    if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, 256, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        ctx_free_all(c);
+        return fail(VR_ERROR_DEVICE, std::string("call context: ") + hipGetErrorString(e));
+    }
+    c->error = (int32_t*)(c->queue + 1);
+    std::lock_guard<std::mutex> g(s->ctx_mutex);
+    s->ctx_all.push_back(c);
+    *out = c;
+    return VR_OK;
+}
+
+void ctx_release(vr_scene* s, CallCtx* c) {
+    std::lock_guard<std::mutex> g(s->ctx_mutex);
+    s->ctx_free.push_back(c);
+}
+
+struct CtxLease {  // RAII hand-back
+    vr_scene* s;
+    CallCtx* c = nullptr;
+    explicit CtxLease(vr_scene* sc) : s(sc) {}
+    ~CtxLease() {
+        if (c) ctx_release(s, c);
+    }
+};
+
+// The sticky error word of `stream` (created zeroed on first use, on that stream).
+int stream_slot(vr_scene* s, void* stream, int32_t** out) {
+    std::lock_guard<std::mutex> g(s->slot_mutex);
+    auto it = s->stream_slots.find(stream);
+    if (it != s->stream_slots.end()) {
+        *out = it->second;
+        return VR_OK;
+    }
+    int32_t* p = nullptr;
+    VR_HIP(hipMalloc(&p, 256));
+    const hipError_t e = hipMemsetAsync(p, 0, 256, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return fail(VR_ERROR_DEVICE, std::string("error slot: ") + hipGetErrorString(e));
+    }
+    s->stream_slots.emplace(stream, p);
+    *out = p;
+    return VR_OK;
+}
 
 }  // namespace
 
@@ -748,6 +850,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     if (!s) return fail(VR_ERROR_OUT_OF_MEMORY, "scene allocation failed");
     s->device = device;
     s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
+    if (const char* fo = getenv("VR_FAULT_SINGULAR_OBJECT")) s->fault_object = (int32_t)atoi(fo);
     s->camera[0] = desc->camera_location.x;
     s->camera[1] = desc->camera_location.y;
     s->camera[2] = desc->camera_location.z;
@@ -1005,14 +1108,11 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
 
 void vr_scene_destroy(vr_scene* s) {
     if (!s) return;
-    if (s->d_block || s->staging) {
+    if (s->d_block || !s->ctx_all.empty() || !s->stream_slots.empty()) {
         (void)hipSetDevice(s->device);
-        if (s->staging_free) {
-            (void)hipEventSynchronize(s->staging_free);
-            (void)hipEventDestroy(s->staging_free);
-        }
-        if (s->staging) (void)hipFree(s->staging);
-        if (s->d_queue) (void)hipFree(s->d_queue);
+        for (CallCtx* c : s->ctx_all) ctx_free_all(c);  // waits for each context's last work
+        // (the streams may be gone by now: hipFree waits for the device instead)
+        for (auto& kv : s->stream_slots) (void)hipFree(kv.second);
         if (s->d_block) (void)hipFree(s->d_block);
     }
     delete s;
@@ -1052,9 +1152,10 @@ int vr_scene_bvh_leaf_order(const vr_scene* s, uint32_t mesh, uint64_t* out) {
 }
 
 namespace {
-// Enqueue the render of params `p` into `state` on stream `st` in passes that fit the staging
-// buffer (16 B per pixel-sample: the final photon).  Caller holds s->staging_mutex.
-// Per-pass events of a timed launch: render kernel [start, mid), ordered reduce [mid, end).
+// Enqueue the render of params `p` into `state` on stream `st`, in passes that fit the context's
+// staging buffer (16 B per pixel-sample: the final photon).  `err` is the device word the kernel
+// flags a singular shading basis in.  Per-pass events of a timed launch: render kernel
+// [start, mid), ordered reduce [mid, end).
 struct PassEvents {
     std::vector<hipEvent_t> ev;
     ~PassEvents() {
@@ -1068,41 +1169,36 @@ struct PassEvents {
     }
 };
 
-int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStream_t st, bool counting,
-                   bool recording, void* records, unsigned long long* counters, unsigned long long* wg_times,
-                   PassEvents* timing = nullptr) {
+int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* state, hipStream_t st, int32_t* err,
+                   bool counting, bool recording, void* records, unsigned long long* counters,
+                   unsigned long long* wg_times, PassEvents* timing = nullptr) {
     const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
     const uint64_t npix = tw * th;
     if (npix == 0 || p->spp == 0) return VR_OK;
     size_t free_b = 0, total_b = 0;
     VR_HIP(hipMemGetInfo(&free_b, &total_b));
-    const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + s->staging_bytes) / 2);
+    const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + c->staging_bytes) / 2);
     uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (16 * npix)));
     // the kernel decodes work items with 32-bit block indices: (8x8 blocks) x samples < 2^32
     if (((tw + 7) / 8) * ((th + 7) / 8) * pass >= (1ull << 32))
         return fail(VR_ERROR_UNSUPPORTED, "too many pixel blocks x samples in one launch (2^32)");
-    const size_t need = (size_t)(16 * npix * pass);
-    // previous users of the staging buffer must be done before it is reused or resized
-    VR_HIP(hipStreamWaitEvent(st, s->staging_free, 0));
-    if (need > s->staging_bytes) {
-        VR_HIP(hipEventSynchronize(s->staging_free));
-        if (s->staging) VR_HIP(hipFree(s->staging));
-        s->staging = nullptr;
-        s->staging_bytes = 0;
-        VR_HIP(hipMalloc(&s->staging, need));
-        s->staging_bytes = need;
-    }
+    // the context's previous user (possibly on another stream) must be done with its buffers
+    VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    int rc = ctx_grow(&c->staging, &c->staging_bytes, (size_t)(16 * npix * pass), c->done);
+    if (rc) return rc;
     for (uint64_t done = 0; done < p->spp; done += pass) {
         vr_render_params q = *p;
         q.spp = (uint32_t)std::min<uint64_t>(pass, p->spp - done);
         q.first_sample = p->first_sample + done;
         q.accumulate = (done > 0 || p->accumulate) ? 1u : 0u;
         vr::RenderArgs a = make_args(s, &q, state);
-        a.staging = (double*)s->staging;
+        a.staging = (double*)c->staging;
+        a.queue = c->queue;
+        a.error_flag = err;
         a.records = records;
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;
-        VR_HIP(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), st));
+        VR_HIP(hipMemsetAsync(c->queue, 0, sizeof(unsigned long long), st));
         hipEvent_t mid = nullptr;
         if (timing) {
             hipEvent_t start = timing->add();
@@ -1113,7 +1209,7 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
         // LDS stack entries: the 4-wide walk's, and the binary walk's for Whitted shadow rays
         const int stack = s->dev.integrator == 1 ? std::max(stack_depth(s), wide_stack_depth(s)) : wide_stack_depth(s);
         int lr = vr::launch_render(a, stack, counting, recording, s->dark0, s->mats ? s->mats : 3,
-                                    std::max(1, s->cu_count) * 3, st, mid);
+                                   std::max(1, s->cu_count) * 3, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {
             hipEvent_t end = timing->add();
@@ -1121,7 +1217,19 @@ int enqueue_passes(vr_scene* s, const vr_render_params* p, double* state, hipStr
             VR_HIP(hipEventRecord(end, st));
         }
     }
-    VR_HIP(hipEventRecord(s->staging_free, st));
+    VR_HIP(hipEventRecord(c->done, st));
+    return VR_OK;
+}
+
+// Scratch of a host-buffer call: device records (64 B per pixel) then the host layout
+// (88 B per pixel: colour, colour_sum, colour_bias, weight, weight_bias back to back).
+int host_call_scratch(CallCtx* c, uint64_t npix, size_t extra, double** state, double** planar, void** rest) {
+    const size_t rec = (npix * 64 + 255) & ~size_t(255), pl = (npix * 88 + 255) & ~size_t(255);
+    int rc = ctx_grow(&c->scratch, &c->scratch_bytes, rec + pl + extra, c->done);
+    if (rc) return rc;
+    *state = (double*)c->scratch;
+    if (planar) *planar = (double*)((char*)c->scratch + rec);
+    if (rest) *rest = (char*)c->scratch + rec + pl;
     return VR_OK;
 }
 }  // namespace
@@ -1134,79 +1242,97 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     VR_HIP(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
     vr_scene* ms = const_cast<vr_scene*>(s);
-    vr::RenderArgs a = make_args(s, p, state);
     const bool counting = (launch_flags & VR_LAUNCH_COUNTERS) != 0;
     const bool timed = (launch_flags & VR_LAUNCH_TIMED) != 0 || counting;
+    int32_t* slot = nullptr;
+    rc = stream_slot(ms, stream, &slot);
+    if (rc) return rc;
     std::unique_lock<std::mutex> lock(ms->counter_mutex, std::defer_lock);
     // diagnostic (tools): with counters, VR_WG_TIMES_PATH receives per-workgroup start/end stamps
     const char* wg_path = counting ? getenv("VR_WG_TIMES_PATH") : nullptr;
     CallScratch wg;
     const uint64_t blocks = (uint64_t)std::max(1, s->cu_count) * 3;  // persistent grid limit
+    unsigned long long* counters = nullptr;
     if (counting) {
         lock.lock();
         VR_HIP(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long) * vr::kCntCount, st));
-        a.counters = s->d_counters;
-        if (wg_path) {
-            VR_HIP(hipMalloc(&wg.ptr, blocks * 2 * sizeof(unsigned long long)));
-            a.wg_times = (unsigned long long*)wg.ptr;
-        }
+        counters = s->d_counters;
+        if (wg_path) VR_HIP(hipMalloc(&wg.ptr, blocks * 2 * sizeof(unsigned long long)));
     }
     PassEvents pe;
     {
-        std::lock_guard<std::mutex> g(ms->staging_mutex);
-        int er = enqueue_passes(ms, p, state, st, counting, false, nullptr, a.counters, a.wg_times,
-                                timed ? &pe : nullptr);
-        if (er) return er;
+        CtxLease L(ms);
+        rc = ctx_acquire(ms, &L.c);
+        if (rc) return rc;
+        rc = enqueue_passes(ms, L.c, p, state, st, slot, counting, false, nullptr, counters,
+                            (unsigned long long*)wg.ptr, timed ? &pe : nullptr);
+        if (rc) return rc;
     }
-    if (timed) {
-        float render_ms = 0.f, reduce_ms = 0.f;
-        if (!pe.ev.empty()) VR_HIP(hipEventSynchronize(pe.ev.back()));
-        for (size_t i = 0; i + 3 <= pe.ev.size(); i += 3) {
-            float x = 0.f, y = 0.f;
-            VR_HIP(hipEventElapsedTime(&x, pe.ev[i], pe.ev[i + 1]));
-            VR_HIP(hipEventElapsedTime(&y, pe.ev[i + 1], pe.ev[i + 2]));
-            render_ms += x;
-            reduce_ms += y;
+    if (!timed) return VR_OK;  // errors of this launch: vr_stream_check_error(scene, stream)
+    float render_ms = 0.f, reduce_ms = 0.f;
+    if (!pe.ev.empty()) VR_HIP(hipEventSynchronize(pe.ev.back()));
+    for (size_t i = 0; i + 3 <= pe.ev.size(); i += 3) {
+        float x = 0.f, y = 0.f;
+        VR_HIP(hipEventElapsedTime(&x, pe.ev[i], pe.ev[i + 1]));
+        VR_HIP(hipEventElapsedTime(&y, pe.ev[i + 1], pe.ev[i + 2]));
+        render_ms += x;
+        reduce_ms += y;
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->kernel_ms = render_ms;
+        stats->reduce_ms = reduce_ms;
+        stats->passes = (uint32_t)(pe.ev.size() / 3);
+        stats->timed = 1;
+    }
+    if (counting) {
+        unsigned long long c[vr::kCntCount];
+        VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+        if (const char* cp = getenv("VR_COUNTERS_PATH")) {  // diagnostic: the raw counter array
+            if (FILE* f = std::fopen(cp, "wb")) {
+                std::fwrite(c, sizeof c, 1, f);
+                std::fclose(f);
+            }
+        }
+        if (wg_path && wg.ptr) {
+            std::vector<unsigned long long> t(blocks * 2);
+            VR_HIP(hipMemcpy(t.data(), wg.ptr, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            if (FILE* f = std::fopen(wg_path, "wb")) {
+                std::fwrite(t.data(), sizeof(unsigned long long), t.size(), f);
+                std::fclose(f);
+            }
         }
         if (stats) {
-            std::memset(stats, 0, sizeof *stats);
-            stats->kernel_ms = render_ms;
-            stats->reduce_ms = reduce_ms;
-            stats->passes = (uint32_t)(pe.ev.size() / 3);
-            stats->timed = 1;
+            stats->box_tests = c[vr::kCntBoxTests];
+            stats->node_visits = c[vr::kCntNodeVisits];
+            stats->triangle_tests = c[vr::kCntTriangleTests];
+            stats->rays = c[vr::kCntRays];
+            stats->shaded_triangle_hits = c[vr::kCntShadedTriangles];
+            stats->samples = c[vr::kCntSamples];
+            stats->traversal_slots = c[vr::kCntTraversalSlots];
+            stats->path_loop_slots = c[vr::kCntOuterSlots];
+            stats->exact_box_tests = c[vr::kCntExactBoxes];
         }
-        if (counting) {
-            unsigned long long c[vr::kCntCount];
-            VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
-            if (const char* cp = getenv("VR_COUNTERS_PATH")) {  // diagnostic: the raw counter array
-                if (FILE* f = std::fopen(cp, "wb")) {
-                    std::fwrite(c, sizeof c, 1, f);
-                    std::fclose(f);
-                }
-            }
-            if (wg_path && wg.ptr) {
-                std::vector<unsigned long long> t(blocks * 2);
-                VR_HIP(hipMemcpy(t.data(), wg.ptr, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-                if (FILE* f = std::fopen(wg_path, "wb")) {
-                    std::fwrite(t.data(), sizeof(unsigned long long), t.size(), f);
-                    std::fclose(f);
-                }
-            }
-            if (stats) {
-                stats->box_tests = c[vr::kCntBoxTests];
-                stats->node_visits = c[vr::kCntNodeVisits];
-                stats->triangle_tests = c[vr::kCntTriangleTests];
-                stats->rays = c[vr::kCntRays];
-                stats->shaded_triangle_hits = c[vr::kCntShadedTriangles];
-                stats->samples = c[vr::kCntSamples];
-                stats->traversal_slots = c[vr::kCntTraversalSlots];
-                stats->path_loop_slots = c[vr::kCntOuterSlots];
-                stats->exact_box_tests = c[vr::kCntExactBoxes];
-            }
-        }
-        return read_and_clear_error(s, st);
     }
-    return VR_OK;
+    return read_and_clear_error(slot, st);
+}
+
+int vr_stream_check_error(const vr_scene* s, void* stream) {
+    if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
+    if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
+    VR_HIP(hipSetDevice(s->device));
+    int32_t* slot = nullptr;
+    {
+        vr_scene* ms = const_cast<vr_scene*>(s);
+        std::lock_guard<std::mutex> g(ms->slot_mutex);
+        auto it = ms->stream_slots.find(stream);
+        if (it != ms->stream_slots.end()) slot = it->second;
+    }
+    if (!slot) {  // nothing of this scene was ever launched on the stream
+        VR_HIP(hipStreamSynchronize((hipStream_t)stream));
+        return VR_OK;
+    }
+    return read_and_clear_error(slot, (hipStream_t)stream);
 }
 
 int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation_buffer* buf) {
@@ -1219,38 +1345,38 @@ int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation
     const uint64_t n = tw * th;
     if (n == 0) return VR_OK;
     VR_HIP(hipSetDevice(s->device));
-    CallScratch cs;
-    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
-    std::vector<double> host(n * 8, 0.0);
-    if (p->accumulate) {
-        for (uint64_t i = 0; i < n; ++i) {
-            for (int k = 0; k < 3; ++k) {
-                host[8 * i + k] = buf->colour_sum[3 * i + k];
-                host[8 * i + 3 + k] = buf->colour_bias[3 * i + k];
-            }
-            host[8 * i + 6] = buf->weight[i];
-            host[8 * i + 7] = buf->weight_bias[i];
-        }
-    }
-    VR_HIP(hipMalloc(&cs.ptr, n * 8 * sizeof(double)));
-    VR_HIP(hipMemcpyAsync(cs.ptr, host.data(), n * 8 * sizeof(double), hipMemcpyHostToDevice, cs.stream));
-    rc = vr_render_tile_device(s, p, (double*)cs.ptr, cs.stream, 0, nullptr);
+    vr_scene* ms = const_cast<vr_scene*>(s);
+    CtxLease L(ms);
+    rc = ctx_acquire(ms, &L.c);
     if (rc) return rc;
-    VR_HIP(hipMemcpyAsync(host.data(), cs.ptr, n * 8 * sizeof(double), hipMemcpyDeviceToHost, cs.stream));
-    VR_HIP(hipStreamSynchronize(cs.stream));
-    rc = read_and_clear_error(s, cs.stream);
-    for (uint64_t i = 0; i < n; ++i) {
-        const double w = host[8 * i + 6];
-        const double inv = 1.0 / w;  // accumulation_buffer.rs:59
-        for (int k = 0; k < 3; ++k) {
-            buf->colour_sum[3 * i + k] = host[8 * i + k];
-            buf->colour_bias[3 * i + k] = host[8 * i + 3 + k];
-            buf->colour[3 * i + k] = w != 0.0 ? host[8 * i + k] * inv : 0.0;
-        }
-        buf->weight[i] = w;
-        buf->weight_bias[i] = host[8 * i + 7];
+    CallCtx* c = L.c;
+    const hipStream_t st = c->stream;
+    VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    double *state = nullptr, *planar = nullptr;
+    rc = host_call_scratch(c, n, 0, &state, &planar, nullptr);
+    if (rc) return rc;
+    const size_t b3 = n * 3 * sizeof(double), b1 = n * sizeof(double);
+    if (p->accumulate) {  // continue update_pixel from the caller's buffer
+        VR_HIP(hipMemcpyAsync(planar + 3 * n, buf->colour_sum, b3, hipMemcpyHostToDevice, st));
+        VR_HIP(hipMemcpyAsync(planar + 6 * n, buf->colour_bias, b3, hipMemcpyHostToDevice, st));
+        VR_HIP(hipMemcpyAsync(planar + 9 * n, buf->weight, b1, hipMemcpyHostToDevice, st));
+        VR_HIP(hipMemcpyAsync(planar + 10 * n, buf->weight_bias, b1, hipMemcpyHostToDevice, st));
+        const int e = vr::launch_buffer_convert(planar, state, n, 0, st);
+        if (e) return fail(VR_ERROR_DEVICE, std::string("buffer import: ") + hipGetErrorString((hipError_t)e));
+    } else {  // AccumulationBuffer::new
+        VR_HIP(hipMemsetAsync(state, 0, n * 64, st));
     }
-    return rc;
+    rc = enqueue_passes(ms, c, p, state, st, c->error, false, false, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    const int e = vr::launch_buffer_convert(state, planar, n, 1, st);
+    if (e) return fail(VR_ERROR_DEVICE, std::string("buffer export: ") + hipGetErrorString((hipError_t)e));
+    VR_HIP(hipMemcpyAsync(buf->colour, planar, b3, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipMemcpyAsync(buf->colour_sum, planar + 3 * n, b3, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipMemcpyAsync(buf->colour_bias, planar + 6 * n, b3, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipMemcpyAsync(buf->weight, planar + 9 * n, b1, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipMemcpyAsync(buf->weight_bias, planar + 10 * n, b1, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipEventRecord(c->done, st));
+    return read_and_clear_error(c->error, st);  // synchronises the call's stream
 }
 
 int vr_partial_render_scene(const vr_scene* s, vr_tile tile, uint64_t height, uint64_t width,
@@ -1275,23 +1401,26 @@ int vr_render_samples(const vr_scene* s, const vr_render_params* p, vr_sample_re
     const uint64_t n = tw * th;
     if (n == 0 || p->spp == 0) return VR_OK;
     VR_HIP(hipSetDevice(s->device));
-    CallScratch cs, rec;
-    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
-    VR_HIP(hipMalloc(&cs.ptr, n * 8 * sizeof(double)));
-    VR_HIP(hipMemsetAsync(cs.ptr, 0, n * 8 * sizeof(double), cs.stream));
+    vr_scene* ms = const_cast<vr_scene*>(s);
+    CtxLease L(ms);
+    rc = ctx_acquire(ms, &L.c);
+    if (rc) return rc;
+    CallCtx* c = L.c;
+    const hipStream_t st = c->stream;
+    VR_HIP(hipStreamWaitEvent(st, c->done, 0));
     const size_t rec_bytes = n * p->spp * sizeof(vr_sample_record);
-    VR_HIP(hipMalloc(&rec.ptr, rec_bytes));
+    double* state = nullptr;
+    void* rec = nullptr;
+    rc = host_call_scratch(c, n, rec_bytes, &state, nullptr, &rec);
+    if (rc) return rc;
+    VR_HIP(hipMemsetAsync(state, 0, n * 64, st));
     vr_render_params q = *p;
     q.accumulate = 0;
-    {
-        vr_scene* ms = const_cast<vr_scene*>(s);
-        std::lock_guard<std::mutex> g(ms->staging_mutex);
-        int er = enqueue_passes(ms, &q, (double*)cs.ptr, cs.stream, false, true, rec.ptr, nullptr, nullptr);
-        if (er) return er;
-    }
-    VR_HIP(hipMemcpyAsync(out, rec.ptr, rec_bytes, hipMemcpyDeviceToHost, cs.stream));
-    VR_HIP(hipStreamSynchronize(cs.stream));
-    return read_and_clear_error(s, cs.stream);
+    rc = enqueue_passes(ms, c, &q, state, st, c->error, false, true, rec, nullptr, nullptr);
+    if (rc) return rc;
+    VR_HIP(hipMemcpyAsync(out, rec, rec_bytes, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipEventRecord(c->done, st));
+    return read_and_clear_error(c->error, st);
 }
 
 int vr_trace_rays(const vr_scene* s, uint64_t n, const double* origins, const double* directions,
@@ -1300,24 +1429,52 @@ int vr_trace_rays(const vr_scene* s, uint64_t n, const double* origins, const do
     if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
     if (n == 0) return VR_OK;
     VR_HIP(hipSetDevice(s->device));
-    CallScratch cs;
-    VR_HIP(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    vr_scene* ms = const_cast<vr_scene*>(s);
+    CtxLease L(ms);
+    int rc = ctx_acquire(ms, &L.c);
+    if (rc) return rc;
+    CallCtx* c = L.c;
+    const hipStream_t st = c->stream;
+    VR_HIP(hipStreamWaitEvent(st, c->done, 0));
     const size_t in_bytes = n * 3 * sizeof(double), out_bytes = n * sizeof(vr_hit_record);
-    VR_HIP(hipMalloc(&cs.ptr, 2 * in_bytes + out_bytes));
-    char* b = (char*)cs.ptr;
-    VR_HIP(hipMemcpyAsync(b, origins, in_bytes, hipMemcpyHostToDevice, cs.stream));
-    VR_HIP(hipMemcpyAsync(b + in_bytes, directions, in_bytes, hipMemcpyHostToDevice, cs.stream));
-    VR_HIP(hipMemsetAsync(b + 2 * in_bytes, 0, out_bytes, cs.stream));
+    rc = ctx_grow(&c->scratch, &c->scratch_bytes, 2 * in_bytes + out_bytes, c->done);
+    if (rc) return rc;
+    char* b = (char*)c->scratch;
+    VR_HIP(hipMemcpyAsync(b, origins, in_bytes, hipMemcpyHostToDevice, st));
+    VR_HIP(hipMemcpyAsync(b + in_bytes, directions, in_bytes, hipMemcpyHostToDevice, st));
+    VR_HIP(hipMemsetAsync(b + 2 * in_bytes, 0, out_bytes, st));
     vr::TraceArgs a{};
     a.scene = s->dev;
     a.n = n;
     a.origins = (const double*)b;
     a.directions = (const double*)(b + in_bytes);
     a.out = b + 2 * in_bytes;
-    int lr = vr::launch_trace(a, stack_depth(s), cs.stream);
+    int lr = vr::launch_trace(a, stack_depth(s), st);
     if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
-    VR_HIP(hipMemcpyAsync(out, b + 2 * in_bytes, out_bytes, hipMemcpyDeviceToHost, cs.stream));
-    VR_HIP(hipStreamSynchronize(cs.stream));
+    VR_HIP(hipMemcpyAsync(out, b + 2 * in_bytes, out_bytes, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipEventRecord(c->done, st));
+    VR_HIP(hipStreamSynchronize(st));
+    return VR_OK;
+}
+
+int vr_merge_tile(vr_accumulation_buffer* dst, vr_tile t, const vr_accumulation_buffer* src) {
+    if (!dst || !src || !dst->colour || !dst->weight || !src->colour || !src->weight)
+        return fail(VR_ERROR_INVALID_ARGUMENT, "null buffer");
+    // accumulation_buffer.rs:63-64 assert the tile size; Array2D indexing asserts the bounds
+    if (t.end_column < t.start_column || t.end_row < t.start_row || t.end_column > dst->width ||
+        t.end_row > dst->height || src->width != t.end_column - t.start_column ||
+        src->height != t.end_row - t.start_row)
+        return fail(VR_ERROR_INVALID_ARGUMENT, "merge_tile: tile does not match the buffers");
+    for (uint64_t i = 0; i < src->height; ++i) {
+        for (uint64_t j = 0; j < src->width; ++j) {
+            const uint64_t d = (t.start_row + i) * dst->width + (t.start_column + j), q = i * src->width + j;
+            const double w1 = dst->weight[d], w2 = src->weight[q];
+            const double inv = 1.0 / (w1 + w2);
+            for (int k = 0; k < 3; ++k)
+                dst->colour[3 * d + k] = (dst->colour[3 * d + k] * w1 + src->colour[3 * q + k] * w2) * inv;
+            dst->weight[d] = w1 + w2;
+        }
+    }
     return VR_OK;
 }
 

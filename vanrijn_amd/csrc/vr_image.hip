@@ -69,6 +69,47 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const double* src, int fro
 
 }  // namespace dev
 
+namespace dev {
+// Host AccumulationBuffer layout (accumulation_buffer.rs:6-12, include/vanrijn_amd.h) <-> the
+// device records (8 f64 per pixel).  planar = [colour 3n | colour_sum 3n | colour_bias 3n |
+// weight n | weight_bias n] doubles, so one host array is one contiguous copy.
+__global__ __launch_bounds__(256) void export_buffer_kernel(const double* __restrict__ state, uint64_t npix,
+                                                            double* __restrict__ planar) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    const double* r = state + p * 8;
+    const double w = r[6];
+    const double inv = 1.0 / w;  // accumulation_buffer.rs:59: colour = sum * (1 / weight)
+    for (int k = 0; k < 3; ++k) {
+        planar[3 * p + k] = w != 0.0 ? r[k] * inv : 0.0;
+        planar[3 * npix + 3 * p + k] = r[k];
+        planar[6 * npix + 3 * p + k] = r[3 + k];
+    }
+    planar[9 * npix + p] = w;
+    planar[10 * npix + p] = r[7];
+}
+__global__ __launch_bounds__(256) void import_buffer_kernel(const double* __restrict__ planar, uint64_t npix,
+                                                            double* __restrict__ state) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    double* r = state + p * 8;
+    for (int k = 0; k < 3; ++k) {
+        r[k] = planar[3 * npix + 3 * p + k];
+        r[3 + k] = planar[6 * npix + 3 * p + k];
+    }
+    r[6] = planar[9 * npix + p];
+    r[7] = planar[10 * npix + p];
+}
+}  // namespace dev
+
+int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_planar, void* stream) {
+    if (npix == 0) return 0;
+    const dim3 grid((unsigned)((npix + 255) / 256)), block(256);
+    if (to_planar) hipLaunchKernelGGL(dev::export_buffer_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
+    else hipLaunchKernelGGL(dev::import_buffer_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
+    return (int)hipGetLastError();
+}
+
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream) {
     if (npix == 0) return 0;
     hipLaunchKernelGGL(dev::tonemap_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,

@@ -135,7 +135,7 @@ struct RenderArgs {
     uint32_t grab;                // items a wave takes from the queue per atomic (0: exactly its need)
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
-    uint32_t pad4;
+    int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
     // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
     double film[4];
@@ -148,7 +148,7 @@ struct RenderArgs {
     void* records;             // vr_sample_record* (record variant) or nullptr
     unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
     unsigned long long* wg_times;  // counting variant: [blocks][2] s_memrealtime at start / end, or nullptr
-    int32_t* error_flag;
+    int32_t* error_flag;          // this call's error word (a singular shading basis sets it)
 };
 
 struct TraceArgs {
@@ -183,6 +183,9 @@ int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool r
                   int grid_limit, void* stream, void* mid_event = nullptr);
 // vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
+// vr_image.hip: device records (8 f64 per pixel) <-> the host AccumulationBuffer's five arrays laid
+// out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read)
+int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_planar, void* stream);
 // vr_build.hip: one mesh's BVH on the device (same nodes and leaf order as the host build)
 int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
                      Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,

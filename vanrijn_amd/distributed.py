@@ -7,22 +7,52 @@ the per-pixel accumulation records (8 f64: sum XYZ, Kahan bias XYZ, weight, weig
 summed onto rank 0 with one collective (RCCL over xGMI on MI355X, gloo on CPU in the tests).
 Summing records merges disjoint sample sets the way AccumulationBuffer::merge_tile's weighted
 blend does (accumulation_buffer.rs:62-85): mean = sum(colour_sum) / sum(weight).
+
+`frame_step` is the one step both bench.py (RCCL, HIP renderer) and tests/test_distributed.py
+(gloo, the oracle standing in for the renderer) run, so the CPU tests exercise bench.py's logic.
 """
 import torch
 import torch.distributed as dist
 
 RECORD = 8  # f64 per pixel
+BIAS_COLUMNS = (3, 4, 5, 7)  # Kahan compensations of the XYZ sums and of the weight
+
+
+def world_info(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
 
 
 def first_sample(step, rank, world, spp):
-    """First sample index of `rank`'s shard in frame `step`."""
+    """First sample index of `rank`'s shard in frame `step` (shards of `spp` samples per pixel)."""
     return (step * world + rank) * spp
 
 
+def shard_spp(total_spp, world, split):
+    """Samples per pixel one rank renders per frame: the whole `total_spp` (weak scaling, every GPU
+    renders a full frame's worth) or `total_spp / world` (strong scaling: SURVEY.md 8(e)'s
+    spp-split of one frame, C4 / C5)."""
+    if not split:
+        return total_spp
+    if total_spp % world:
+        raise ValueError(f"{total_spp} spp do not split evenly over {world} ranks")
+    return total_spp // world
+
+
 def reduce_records(state: torch.Tensor, dst=0, group=None):
-    """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path).
+
+    The summed Kahan compensations belong to no single update_pixel sequence
+    (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
+    reduced state then starts a fresh compensated sum from the merged totals."""
+    rank, world = world_info(group)
+    if world > 1:
         dist.reduce(state, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if rank == dst:
+            s = state.view(-1, RECORD)
+            s[:, 3:6] = 0.0
+            s[:, 7] = 0.0
     return state
 
 
@@ -33,12 +63,11 @@ def mean_colour(state: torch.Tensor):
     return torch.where(w != 0, s[:, 0:3] * (1.0 / w), torch.zeros_like(s[:, 0:3]))
 
 
-def render_frame(render_shard, step, spp, group=None):
-    """Run one frame on this rank: render_shard(first_sample) -> records tensor, then reduce.
-
-    `render_shard` enqueues (GPU) or computes (CPU) this rank's records for samples
-    [first_sample, first_sample + spp)."""
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    state = render_shard(first_sample(step, rank, world, spp))
-    return reduce_records(state, group=group)
+def frame_step(render_shard, state: torch.Tensor, step, spp, group=None):
+    """One frame on this rank: render_shard(first_sample, state) renders (or enqueues) this rank's
+    `spp` samples per pixel into `state` (fresh records), then the records are reduced onto rank 0.
+    Returns what render_shard returned (launch stats on the GPU)."""
+    rank, world = world_info(group)
+    out = render_shard(first_sample(step, rank, world, spp), state)
+    reduce_records(state, group=group)
+    return out

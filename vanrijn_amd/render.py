@@ -93,13 +93,10 @@ class AccumulationBuffer:
                                      self.weight_buffer.ctypes.data, self.weight_bias_buffer.ctypes.data)
 
     def merge_tile(self, tile: Tile, src: "AccumulationBuffer"):
-        """accumulation_buffer.rs:62-85: weighted blend of the means; weights add."""
-        assert tile.width() == src.width() and tile.height() == src.height()
-        dc = self.colour_buffer[tile.start_row:tile.end_row, tile.start_column:tile.end_column]
-        dw = self.weight_buffer[tile.start_row:tile.end_row, tile.start_column:tile.end_column]
-        w1, w2 = dw[..., None], src.weight_buffer[..., None]
-        dc[...] = (dc * w1 + src.colour_buffer * w2) * (1.0 / (w1 + w2))
-        dw += src.weight_buffer
+        """accumulation_buffer.rs:62-85: weighted blend of the means; weights add (vr_merge_tile,
+        host code in the library; the size asserts become VrError)."""
+        dc, sc = self._c(), src._c()
+        N.check(N.lib().vr_merge_tile(C.byref(dc), tile._c(), C.byref(sc)))
 
     def to_image_rgb_u8(self, device=0) -> "ImageRgbU8":
         """ClampingToneMapper over the XYZ colour buffer (image.rs:166-187), on the GPU."""
@@ -189,6 +186,13 @@ def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample
     N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
                                           C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
     return st.as_dict()
+
+
+def stream_check_error(scene, stream_ptr=None, device=0):
+    """Errors of earlier asynchronous launches of `scene` on a stream (vr_stream_check_error):
+    raises VrError(VR_ERROR_SINGULAR_BASIS) once, then the stream is clean again."""
+    ds = _scene_handle(scene, device)
+    N.check(N.lib().vr_stream_check_error(ds.handle, C.c_void_p(stream_ptr or 0)))
 
 
 def resolve_state(state):
