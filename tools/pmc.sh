@@ -11,6 +11,7 @@ OUT=gpurun_out/pmc/$NAME
 mkdir -p "$OUT"
 ARGS="${PMC_BENCH_ARGS:-} --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in"
 echo "$ARGS" > "$OUT/args.txt"
+sha256sum vanrijn_amd/lib/libvanrijn_amd.so | cut -d' ' -f1 > "$OUT/lib.sha256"  # the build profiled
 run_pass() {
   local name=$1; shift
   timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run --pmc "$@" -- \
@@ -25,3 +26,4 @@ run_pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
 run_pass tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
 run_pass sq2 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_WR
 run_pass sq3 SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32
+run_pass sq4 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32

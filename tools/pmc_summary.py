@@ -68,8 +68,12 @@ def main():
         per_launch.update(disp[last])
         if last in dur:
             kernel_ns[name] = dur[last]
-    lib = os.path.join(ROOT, "vanrijn_amd", "lib", "libvanrijn_amd.so")
-    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    sha_file = os.path.join(pmc_dir, "lib.sha256")  # written on the box by tools/pmc.sh
+    if os.path.exists(sha_file):
+        sha = open(sha_file).read().strip()
+    else:
+        lib = os.path.join(ROOT, "vanrijn_amd", "lib", "libvanrijn_amd.so")
+        sha = sys.argv[3] if len(sys.argv) > 3 else hashlib.sha256(open(lib, "rb").read()).hexdigest()
     key = bench_key(pmc_dir)
     rec = {"lib_sha256": sha, "config": key, "per_launch": per_launch,
            "kernel_ns": kernel_ns.get("tcc") or max(kernel_ns.values()),

@@ -187,26 +187,22 @@ __global__ void gather_kernel(const double* verts, const double* norms, const ui
 
 // The render kernel's 4-wide tree over a device-built binary tree: one thread per wide node
 // gathers its child boxes from the binary nodes named by the host-made descriptor (desc[8i + k]:
-// binary node * 2 + child for slot k, or -1; desc[8i + 4 + k]: the slot's child link), keeps the
-// f64 box and writes the f32 copy rounded outward (min toward -inf, max toward +inf: the host
-// build's nextafter rule).
-__global__ void fill_wide_kernel(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, Node4x* out4x) {
+// binary node * 2 + child for slot k, or -1; desc[8i + 4 + k]: the slot's child link) and writes
+// them rounded outward to f32 (min toward -inf, max toward +inf: the host build's nextafter rule).
+__global__ void fill_wide_kernel(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     Node4 w;
-    Node4x x;
     for (int k = 0; k < 4; ++k) {
         const int32_t src = desc[8 * i + k];
         w.child[k] = desc[8 * i + 4 + k];
         w.pad[k] = 0;
         for (int j = 0; j < 6; ++j) {
             const double v = src >= 0 ? bin[src >> 1].box[src & 1][j] : NAN;
-            x.box[k][j] = v;
             w.box[k][j] = src < 0 ? NAN : ((j & 1) ? __double2float_ru(v) : __double2float_rd(v));
         }
     }
     out4[i] = w;
-    out4x[i] = x;
 }
 
 }  // namespace build
@@ -339,11 +335,11 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
     return 0;
 }
 
-int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, Node4x* out4x, void* stream) {
+int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream) {
     if (n4 == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(build::fill_wide_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, bin, desc, n4,
-                       out4, out4x);
+                       out4);
     return (int)hipGetLastError();
 }
 

@@ -293,10 +293,8 @@ float round_upper(double v) {
 struct WideBuilder {
     const std::vector<vr::Node>& bin;
     std::vector<vr::Node4>& n4;
-    std::vector<vr::Node4x>& n4x;
     int stack = 0;
-    WideBuilder(const std::vector<vr::Node>& b, std::vector<vr::Node4>& a, std::vector<vr::Node4x>& x)
-        : bin(b), n4(a), n4x(x) {}
+    WideBuilder(const std::vector<vr::Node>& b, std::vector<vr::Node4>& a) : bin(b), n4(a) {}
 
     static double area(const double* b) {
         const double dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
@@ -331,7 +329,6 @@ struct WideBuilder {
         }
         const int32_t me = (int32_t)n4.size();
         n4.emplace_back();
-        n4x.emplace_back();
         int interior = 0;
         for (int k = 0; k < n; ++k) interior += code[k] >= 0;
         const int here = pushed + std::max(0, interior - 1);
@@ -340,13 +337,11 @@ struct WideBuilder {
         for (int k = 0; k < 4; ++k) out[k] = vr::kEmptyChild;
         for (int k = 0; k < n; ++k) out[k] = code[k] >= 0 ? collapse(code[k], here) : code[k];
         vr::Node4& w = n4[me];
-        vr::Node4x& x = n4x[me];
         std::memset(&w, 0, sizeof w);
         for (int k = 0; k < 4; ++k) {
             w.child[k] = out[k];
             for (int j = 0; j < 6; ++j) {
                 const double v = k < n ? box[k][j] : NAN;
-                x.box[k][j] = v;
                 w.box[k][j] = k < n ? ((j & 1) ? round_upper(v) : round_lower(v)) : NAN;
             }
         }
@@ -426,7 +421,6 @@ struct vr_scene {
     std::vector<double> light_dirs;  // Whitted: 3 per light
     std::vector<vr::Node> nodes;
     std::vector<vr::Node4> nodes4;  // the render kernel's 4-wide tree (collapse_wide)
-    std::vector<vr::Node4x> nodes4x;
     int wide_stack = 0;             // deepest traversal stack of the 4-wide tree
     uint64_t wide_count = 0;        // its node count
     std::vector<vr::TriVerts> tris;
@@ -493,8 +487,7 @@ int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     s->nodes4.clear();
-    s->nodes4x.clear();
-    WideBuilder W(nodes, s->nodes4, s->nodes4x);
+    WideBuilder W(nodes, s->nodes4);
     for (auto& b : s->bvhs) b.root4 = b.root >= 0 ? W.collapse(b.root, 0) : b.root;
     s->wide_stack = W.stack;
     s->wide_count = s->nodes4.size();
@@ -520,17 +513,16 @@ int upload(vr_scene* s) {
     // the 4-wide tree has at most one node per binary interior node (device builds collapse after
     // the build, so its arrays are sized by that bound)
     const size_t sz_nodes4 = s->node_count * sizeof(vr::Node4);
-    const size_t sz_nodes4x = s->node_count * sizeof(vr::Node4x);
     const size_t sz_tris = s->tri_count * sizeof(vr::TriVerts);
     const size_t sz_norm = s->tri_count * sizeof(vr::TriNormals);
     const size_t sz_mat = s->materials.size() * sizeof(vr::Material);
     const size_t sz_prim = s->prims.size() * sizeof(vr::Prim);
     const size_t sz_bvh = s->bvhs.size() * sizeof(vr::Bvh);
-    size_t off[9], total = 0;
+    size_t off[8], total = 0;
     const size_t sz_misc = 64 + vr::kCntCount * sizeof(unsigned long long);  // error flag, counters
-    const size_t sizes[9] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh,
-                             sz_misc + 3 * VR_MAX_LIGHTS * sizeof(double), sz_nodes4, sz_nodes4x};
-    for (int i = 0; i < 9; ++i) {
+    const size_t sizes[8] = {sz_nodes, sz_tris, sz_norm, sz_mat, sz_prim, sz_bvh,
+                             sz_misc + 3 * VR_MAX_LIGHTS * sizeof(double), sz_nodes4};
+    for (int i = 0; i < 8; ++i) {
         off[i] = total;
         total += align_up<char>(std::max<size_t>(sizes[i], 1));
     }
@@ -553,7 +545,6 @@ int upload(vr_scene* s) {
     vr::DeviceScene& d = s->dev;
     d.nodes = (const vr::Node*)(base + off[0]);
     d.nodes4 = (const vr::Node4*)(base + off[7]);
-    d.nodes4x = (const vr::Node4x*)(base + off[8]);
     d.tris = (const vr::TriVerts*)(base + off[1]);
     d.normals = (const vr::TriNormals*)(base + off[2]);
     d.materials = (const vr::Material*)(base + off[3]);
@@ -596,7 +587,7 @@ int upload(vr_scene* s) {
             const hipError_t ec = hipMemcpy(d_desc, W.desc.data(), W.desc.size() * sizeof(int32_t), hipMemcpyHostToDevice);
             const int e = ec != hipSuccess ? (int)ec
                                            : vr::device_fill_wide(nodes, d_desc, s->wide_count, (vr::Node4*)(base + off[7]),
-                                                                  (vr::Node4x*)(base + off[8]), cs.stream);
+                                                                  cs.stream);
             const hipError_t es = hipStreamSynchronize(cs.stream);
             (void)hipFree(d_desc);
             if (e || es != hipSuccess) return fail(VR_ERROR_DEVICE, "device wide-tree fill failed");
@@ -606,8 +597,6 @@ int upload(vr_scene* s) {
     }
     if (!s->nodes4.empty()) {
         VR_HIP(hipMemcpy(base + off[7], s->nodes4.data(), s->nodes4.size() * sizeof(vr::Node4), hipMemcpyHostToDevice));
-        VR_HIP(hipMemcpy(base + off[8], s->nodes4x.data(), s->nodes4x.size() * sizeof(vr::Node4x),
-                         hipMemcpyHostToDevice));
     }
     return VR_OK;
 }

@@ -31,8 +31,9 @@ static_assert(sizeof(Node) == 128, "Node must be one 128-B line");
 // boxes are rounded OUTWARD to f32 (each f32 box contains its f64 box); child[c] >= 0: wide node
 // index, child[c] < 0 (and != kEmptyChild): leaf holding triangle ~child[c], whose box is the
 // triangle's own box; kEmptyChild: unused slot.  A box test is decided from this record unless
-// the f32 interval is within its error bound of a tie; then the exact f64 box of the same slot
-// (Node4x, same index) decides.
+// the f32 interval is within its error bound of a tie; then an interior child is descended (a
+// superset box: only extra work) and a leaf child's exact f64 test runs on the triangle's own box,
+// recomputed from its vertices in the leaf round.
 constexpr int32_t kEmptyChild = INT32_MIN;  // ~INT32_MAX: never a triangle (tri_count <= INT32_MAX)
 struct alignas(128) Node4 {
     float box[4][6];   // 96 B: {min x, max x, min y, max y, min z, max z} per child
@@ -40,10 +41,6 @@ struct alignas(128) Node4 {
     int32_t pad[4];    // 16 B -> 128 B, one cache line
 };
 static_assert(sizeof(Node4) == 128, "Node4 must be one 128-B line");
-struct alignas(64) Node4x {
-    double box[4][6];  // 192 B: the exact boxes (read only for f32 tests too close to call)
-};
-static_assert(sizeof(Node4x) == 192, "Node4x must be 192 B");
 
 // Triangle vertices in traversal-BVH leaf order, 80 B for 16-B aligned loads.  `rank` is the
 // triangle's scene-wide position in the REFERENCE tree's in-order leaf sequence (tri_base + leaf
@@ -99,7 +96,6 @@ struct Bvh {
 struct DeviceScene {
     const Node* nodes;     // binary tree (trace / shadow rays)
     const Node4* nodes4;   // 4-wide traversal tree (render kernel)
-    const Node4x* nodes4x;
     const TriVerts* tris;
     const TriNormals* normals;
     const Material* materials;
@@ -191,7 +187,7 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
                      Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
                      int* levels, void* stream);
 // vr_build.hip: Node4 / Node4x records from a device-built binary tree and a host-made descriptor
-int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, Node4x* out4x, void* stream);
+int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);
 

@@ -96,7 +96,6 @@ __device__ __forceinline__ KArgs kargs() {
     return p;
 }
 #define VR_NODES4 (kargs()->scene.nodes4)
-#define VR_NODES4X (kargs()->scene.nodes4x)
 #define VR_TRIS (kargs()->scene.tris)
 
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
@@ -173,10 +172,26 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         if ((double)f < t) f = nextafterf(f, INFINITY);
         cull_far = f;
     };
-    auto test_tri = [&](int tri) {
+    // a queued leaf: its triangle index, bit 31 set when the leaf's f32 box test was too close to
+    // call -- then the exact f64 line test on the triangle's own box (BoundingBox::from_points of
+    // its vertices, triangle.rs:101-105: per axis fmin / fmax in vertex order, the host build's
+    // leaf box bit for bit) decides whether the reference reaches the triangle at all
+    auto test_tri = [&](int e) {
+        const int tri = e & 0x7fffffff;
+        const TriVerts tv = load_tri(VR_TRIS + tri);
+        if (e < 0) {
+            VR_SEC(2);
+            if (COUNT) cnt.exact_boxes++;
+            double bb[6], lo, hi;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                bb[2 * a] = fmin(fmin(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                bb[2 * a + 1] = fmax(fmax(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+            }
+            if (!slab(bb, pre, lo, hi)) return;
+        }
         if (COUNT) cnt.tri_tests++;
         double b[3];
-        const TriVerts tv = load_tri(VR_TRIS + tri);
         const double d = triangle_distance(tv, pre, b);
         if (d < 0.0) return;
         bool take;
@@ -595,7 +610,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
-                uint32_t hm = 0, xm = 0;  // per-child bits: hit (decided in f32), too close to call
+                // per-child bits: descend / queue (f32 hit or too close to call, not culled), and
+                // too close to call.  An interior child too close to call is descended: its box is
+                // a superset of its leaves' boxes, so walking it only costs work (DESIGN.md section
+                // 5); a leaf child too close to call is queued with bit 31 set and its exact f64 box
+                // test runs in the leaf round, beside the triangle test (the f32 bounds tlo / thi
+                // enclose the exact interval either way, so the f32 cull stays conservative)
+                uint32_t hm = 0, xm = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     c[k] = nd.child[k];
@@ -603,18 +624,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     const int r = slab32(nd.box[k], pre32, f[k], g);
                     const bool live = c[k] != kEmptyChild;
                     if (COUNT && live) cnt.box_tests++;
-                    hm |= (live && r == 1 && !(f[k] > cull_far || g < cull_behind)) ? 1u << k : 0u;
-                    xm |= (live && r == 2) ? 1u << k : 0u;
-                }
-                if (xm) { VR_SEC(2); }
-                // too close to call in f32: the exact test and the f64 cull, one inlined copy
-                // run once per undecided child
-                while (xm) {
-                    const int k = __builtin_ctz(xm);
-                    xm &= xm - 1;
-                    if (COUNT) cnt.exact_boxes++;
-                    double lo, hi;
-                    if (slab(VR_NODES4X[node].box[k], pre, lo, hi) && !culled(lo, hi)) hm |= 1u << k;
+                    const bool pass = live && r != 0 && !(f[k] > cull_far || g < cull_behind);
+                    hm |= pass ? 1u << k : 0u;
+                    xm |= (pass && r == 2) ? 1u << k : 0u;
                 }
                 // leaf children: queue their triangles (unconditional LDS writes, the count
                 // advances only for hits; np <= kPend - 4 leaves room for all four)
@@ -623,7 +635,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const bool h = (hm >> k) & 1u;
-                    st_pend[np * 256 + tid] = ~c[k];
+                    st_pend[np * 256 + tid] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
                     np += (h && c[k] < 0) ? 1 : 0;
                     // hit: a finite key (NaN or infinite f32 bounds of exactly-decided children
                     // clamp into range); INFINITY marks "not descended"
