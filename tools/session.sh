@@ -1,7 +1,8 @@
 #!/bin/bash
-# One GPU session: parity tests, a bench line, a rocprofv3 kernel-trace summary, PMC passes.
-#   STEPS="tests bench prof pmc list" TAG=v14 bash tools/session.sh
-# Every GPU step runs under its own time limit and the session stops at the first failure.
+# One GPU session: parity tests, bench lines, rocprofv3 kernel-trace summaries, PMC passes.
+#   STEPS="tests bench prof pmc bench:c5 prof:c5 pmc:c5 list" TAG=v15 bash tools/session.sh
+# A step "name:cN" runs that step on bench.py --config cN (default c3).  Every GPU step runs under
+# its own time limit and the session stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -9,22 +10,32 @@ export TMPDIR=/tmp
 STEPS=${STEPS:-"tests bench prof"}
 TAG=${TAG:-cur}
 BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 1"}
+sha256sum vanrijn_amd/lib/libvanrijn_amd.so > gpurun_out/${TAG}_lib.sha256
 for s in $STEPS; do
-  case $s in
+  step=${s%%:*}; cfg=c3
+  [ "$step" != "$s" ] && cfg=${s#*:}
+  case $step in
     tests)
       timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
           -p no:cacheprovider > gpurun_out/${TAG}_gpu_tests.log 2>&1
       rc=$?; echo "gpu tests rc=$rc"; tail -4 gpurun_out/${TAG}_gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/${TAG}_smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
-      rc=$?; echo "bench rc=$rc"; cut -c 1-400 gpurun_out/${TAG}_bench.json; tail -3 gpurun_out/${TAG}_bench.err ;;
+      if [ "$cfg" = c3 ]; then args="$BENCH_ARGS"; else args="--config $cfg --steps 2 --warmup 1 --no-cpu-baseline --no-drop-in"; fi
+      timeout -k 10 600 python bench.py $args > gpurun_out/${TAG}_bench_$cfg.json 2> gpurun_out/${TAG}_bench_$cfg.err
+      rc=$?; echo "bench $cfg rc=$rc"; cut -c 1-400 gpurun_out/${TAG}_bench_$cfg.json; tail -3 gpurun_out/${TAG}_bench_$cfg.err ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
-          python bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-drop-in > gpurun_out/${TAG}_prof_bench.json \
-          2> gpurun_out/${TAG}_prof.err
-      rc=$?; echo "rocprof rc=$rc" ;;
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_$cfg -o run -- \
+          python bench.py --config $cfg --steps 2 --warmup 0 --no-cpu-baseline --no-drop-in \
+          > gpurun_out/${TAG}_prof_bench_$cfg.json 2> gpurun_out/${TAG}_prof_$cfg.err
+      rc=$?; echo "rocprof $cfg rc=$rc" ;;
     pmc)
-      PMC_NAME=${TAG}_c3 PMC_BENCH_ARGS="--config c3" bash tools/pmc.sh; rc=$? ;;
+      PMC_NAME=${TAG}_$cfg PMC_BENCH_ARGS="--config $cfg" bash tools/pmc.sh; rc=$? ;;
+    cycles)
+      timeout -k 10 300 python tools/cycles.py 64 main > gpurun_out/${TAG}_cycles_main.json 2> gpurun_out/${TAG}_cycles.err
+      rc=$?; echo "cycles rc=$rc" ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1; rc=$?; echo "list rc=$rc" ;;
     *) echo "unknown step $s"; rc=2 ;;
