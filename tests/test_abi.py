@@ -108,3 +108,26 @@ def test_merge_tile_matches_oracle(oracle):
         assert e.code == -1
     else:
         raise AssertionError("mismatched merge_tile must fail")
+
+
+def test_merge_tile_large_tile_threaded(oracle):
+    """A tile large enough to be split over host threads merges exactly like the oracle."""
+    from vanrijn_amd.render import AccumulationBuffer, Tile
+    g = np.random.default_rng(6)
+    W, H = 700, 300
+    dst = AccumulationBuffer(W, H)
+    dst.colour_buffer[...] = g.uniform(0, 2, (H, W, 3))
+    dst.weight_buffer[...] = g.integers(1, 9, (H, W)).astype(float)
+    t = Tile(1, 699, 3, 297)
+    src = AccumulationBuffer(t.width(), t.height())
+    src.colour_buffer[...] = g.uniform(0, 2, (t.height(), t.width(), 3))
+    src.weight_buffer[...] = g.integers(1, 9, (t.height(), t.width())).astype(float)
+    ref_c, ref_w = dst.colour_buffer.copy(), dst.weight_buffer.copy()
+    oracle.lib().orc_merge_tile(W, ref_c.ctypes.data, ref_w.ctypes.data, t.start_row, t.start_column, t.height(),
+                                t.width(), src.colour_buffer.ctypes.data, src.weight_buffer.ctypes.data)
+    for _ in range(3):  # the host pool is reused across calls
+        d = AccumulationBuffer(W, H)
+        d.colour_buffer[...] = dst.colour_buffer
+        d.weight_buffer[...] = dst.weight_buffer
+        d.merge_tile(t, src)
+        assert np.array_equal(d.colour_buffer, ref_c) and np.array_equal(d.weight_buffer, ref_w)

@@ -134,6 +134,20 @@ def test_partial_render_scene_contract(main_pair):
     assert np.allclose(full.colour_buffer[5:13, 3:19], (a.colour_buffer + b.colour_buffer) / 2, rtol=0, atol=1e-15)
 
 
+def test_one_sample_fresh_buffer_fast_path(main_pair):
+    """vr_render_tile with spp 1 into a fresh buffer brings back only colour_sum and derives the other
+    four arrays on the host; it equals update_pixel on an explicit all-zero buffer (the general
+    path: all five arrays through the device) bit for bit."""
+    scene, _ = main_pair
+    H, W = 300, 260  # > 64k pixels: the host expansion runs on several threads
+    t = Tile(0, W, 0, H)
+    fast = render_tile(scene, t, H, W, 1, seed=11, first_sample=5)
+    general = render_tile(scene, t, H, W, 1, seed=11, first_sample=5, accumulate=AccumulationBuffer(W, H))
+    for k in ("colour_sum_buffer", "colour_bias_buffer", "weight_buffer", "weight_bias_buffer", "colour_buffer"):
+        assert np.array_equal(getattr(fast, k), getattr(general, k), equal_nan=True), k
+    assert np.array_equal(fast.weight_buffer, np.ones((H, W)))
+
+
 def test_tile_invariance_and_continuation(main_pair):
     scene, _ = main_pair
     H, W = 48, 40

@@ -1,20 +1,23 @@
 #!/bin/bash
-# A/B two library builds on the GPU box: alternating processes, main 256 spp + bench 32 spp.
-#   bash tools/ab.sh path/to/libA.so path/to/libB.so [rounds]
+# A/B library builds on the GPU box: alternating processes, main 256 spp + bench 32 spp per library.
+#   ROUNDS=3 bash tools/ab.sh path/to/libA.so path/to/libB.so [more libraries ...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-A=$1; B=$2; R=${3:-3}
+R=${ROUNDS:-3}
 : > gpurun_out/ab_libs.jsonl
 for r in $(seq 1 "$R"); do
-  for L in "$A" "$B"; do
+  for L in "$@"; do
     VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene main --spp 256 --reps 2 --variants 0 \
         --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
     rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
-    VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene bench --spp 32 --reps 2 --variants 0 \
-        --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
-    rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
+    if [ "${BENCH_SCENE:-1}" = 1 ]; then
+      VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene bench --spp 32 --reps 2 --variants 0 \
+          --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
+      rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
+    fi
   done
+  echo "round $r done"
 done
 python3 - <<'PY'
 import json, collections
@@ -22,7 +25,7 @@ d = collections.defaultdict(list)
 for line in open("gpurun_out/ab_libs.jsonl"):
     name, js = line.split(" ", 1)
     r = json.loads(js)
-    d[(name, r["scene"])].append(r["median_ms"])
+    d[(r["scene"], name)].append(r["median_ms"])
 for k, v in sorted(d.items()):
     print(k, "median of medians %.3f ms" % sorted(v)[len(v) // 2], ["%.2f" % x for x in v])
 PY

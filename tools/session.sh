@@ -36,6 +36,9 @@ for s in $STEPS; do
     cycles)
       timeout -k 10 300 python tools/cycles.py 64 main > gpurun_out/${TAG}_cycles_main.json 2> gpurun_out/${TAG}_cycles.err
       rc=$?; echo "cycles rc=$rc" ;;
+    dropin)
+      timeout -k 10 400 python tools/dropin.py 1024 32 > gpurun_out/${TAG}_dropin.json 2> gpurun_out/${TAG}_dropin.err
+      rc=$?; echo "dropin rc=$rc"; tail -1 gpurun_out/${TAG}_dropin.json ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1; rc=$?; echo "list rc=$rc" ;;
     *) echo "unknown step $s"; rc=2 ;;

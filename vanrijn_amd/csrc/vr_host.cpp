@@ -12,15 +12,21 @@
 //   ColourXyz::for_wavelength                     src/colour/colour_xyz.rs:22-29, 86-103
 //   load_obj                                      src/mesh.rs:13-88
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -477,7 +483,112 @@ struct CallCtx {
     int32_t* error = nullptr;
     void* scratch = nullptr;  // device records + host-layout buffers of the host-buffer calls
     size_t scratch_bytes = 0;
+    void* pinned = nullptr;  // page-locked host copy of the host-layout buffers (DMA at full PCIe rate)
+    size_t pinned_bytes = 0;
 };
+
+// ---------------------------------------------------------------------------------------------
+// Host threads for the host-buffer entry points: copying the AccumulationBuffer arrays between
+// page-locked staging and the caller's memory, and vr_merge_tile.  88 B per pixel of host memory
+// traffic is ~5 ms per 1024^2 frame on one core -- more than the GPU's share of a 1-spp render.
+// ---------------------------------------------------------------------------------------------
+// the CPUs this process may run on (sched affinity), at most 16 (VR_HOST_THREADS overrides)
+static unsigned host_threads() {
+    static const unsigned n = [] {
+        unsigned c = 0;
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0) c = (unsigned)CPU_COUNT(&set);
+        if (c == 0) c = std::thread::hardware_concurrency();
+        if (const char* e = getenv("VR_HOST_THREADS")) c = (unsigned)atoi(e);
+        return std::max(1u, std::min(c, 16u));
+    }();
+    return n;
+}
+
+// A persistent pool: run(parts, fn) calls fn(0..parts-1) on the pool's threads and the caller's,
+// and returns when all parts are done.  Concurrent callers share the pool (jobs queue FIFO; each
+// caller also works on its own job, so a busy pool never blocks progress).
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool* p = new HostPool(host_threads() - 1);  // never destroyed: threads idle at exit
+        return *p;
+    }
+    void run(unsigned parts, const std::function<void(unsigned)>& fn) {
+        if (parts == 0) return;
+        Job j;
+        j.fn = &fn;
+        j.parts = parts;
+        if (parts > 1 && !threads_.empty()) {
+            std::lock_guard<std::mutex> g(m_);
+            jobs_.push_back(&j);
+            cv_.notify_all();
+        }
+        for (unsigned i; (i = j.next.fetch_add(1)) < parts;) {
+            fn(i);
+            j.done.fetch_add(1);
+        }
+        std::unique_lock<std::mutex> l(m_);
+        for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
+            if (*it == &j) {
+                jobs_.erase(it);
+                break;
+            }
+        done_cv_.wait(l, [&] { return j.done.load() == parts; });
+    }
+
+  private:
+    struct Job {
+        const std::function<void(unsigned)>* fn = nullptr;
+        unsigned parts = 0;
+        std::atomic<unsigned> next{0}, done{0};
+    };
+    explicit HostPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) threads_.emplace_back([this] { work(); });
+    }
+    void work() {
+        std::unique_lock<std::mutex> l(m_);
+        while (true) {
+            cv_.wait(l, [&] { return !jobs_.empty(); });
+            Job* j = jobs_.front();
+            const unsigned i = j->next.fetch_add(1);
+            if (i >= j->parts) {  // every part taken: the job leaves the queue
+                jobs_.pop_front();
+                continue;
+            }
+            l.unlock();
+            (*j->fn)(i);
+            const bool last = j->done.fetch_add(1) + 1 == j->parts;
+            l.lock();
+            if (last) done_cv_.notify_all();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job*> jobs_;
+    std::vector<std::thread> threads_;
+};
+
+// fn(begin, end) over [0, n) in about `host_threads()` pieces of at least `grain`
+static void parallel_range(uint64_t n, uint64_t grain, const std::function<void(uint64_t, uint64_t)>& fn) {
+    const uint64_t pieces = std::max<uint64_t>(1, std::min<uint64_t>(host_threads(), n / std::max<uint64_t>(1, grain)));
+    if (pieces <= 1) {
+        fn(0, n);
+        return;
+    }
+    const uint64_t step = (n + pieces - 1) / pieces;
+    HostPool::get().run((unsigned)pieces, [&](unsigned i) {
+        const uint64_t b = std::min(n, (uint64_t)i * step), e = std::min(n, b + step);
+        if (b < e) fn(b, e);
+    });
+}
+
+// copy `bytes` in parallel (host memory bandwidth, not one core's)
+static void parallel_copy(void* dst, const void* src, size_t bytes) {
+    parallel_range(bytes, (size_t)1 << 20, [&](uint64_t b, uint64_t e) {
+        std::memcpy((char*)dst + b, (const char*)src + b, e - b);
+    });
+}
 
 namespace {
 
@@ -640,7 +751,18 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     const char* ts = getenv("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end
     a.tail_samples = ts ? (uint32_t)std::max(0, atoi(ts)) : 0u;
     const char* gr = getenv("VR_GRAB");  // tuning hook: items per queue atomic
-    a.grab = gr ? (uint32_t)std::max(0, atoi(gr)) : 512u;
+    if (gr) {
+        a.grab = (uint32_t)std::max(0, atoi(gr));
+    } else {
+        // 512 items per atomic keeps the queue counter cold on full frames; a small launch (one
+        // sample per pixel, vr_partial_render_scene) would hand 512 items to a few waves and leave
+        // the rest of the chip idle (1 spp of 1024^2: 1.9 ms at 512), so every wave gets about 16
+        // slices, in multiples of 64 (one item per lane)
+        const uint64_t items = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64 * std::max(1u, p->spp);
+        const uint64_t waves = (uint64_t)std::max(1, s->cu_count) * 3 * 4;
+        const uint64_t g = items / (waves * 16) / 64 * 64;
+        a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(64, g));
+    }
     const char* lt = getenv("VR_LEAF_THRESHOLD");  // tuning hooks
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 64u;
     const char* ls = getenv("VR_LEAF_STALL");
@@ -694,6 +816,19 @@ int ctx_grow(void** ptr, size_t* have, size_t need, hipEvent_t done) {
     return VR_OK;
 }
 
+// Grow the context's page-locked host buffer (its previous contents are only read by the host
+// within the call that filled it, so no device wait is needed beyond the context's `done`).
+int ctx_grow_pinned(CallCtx* c, size_t need) {
+    if (need <= c->pinned_bytes) return VR_OK;
+    VR_HIP(hipEventSynchronize(c->done));
+    if (c->pinned) VR_HIP(hipHostFree(c->pinned));
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+    VR_HIP(hipHostMalloc(&c->pinned, need, hipHostMallocDefault));
+    c->pinned_bytes = need;
+    return VR_OK;
+}
+
 void ctx_free_all(CallCtx* c) {
     if (c->done) {
         (void)hipEventSynchronize(c->done);
@@ -702,6 +837,7 @@ void ctx_free_all(CallCtx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->staging) (void)hipFree(c->staging);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->queue) (void)hipFree(c->queue);
     delete c;
 }
@@ -720,7 +856,9 @@ int ctx_acquire(vr_scene* s, CallCtx** out) {
     CallCtx* c = new (std::nothrow) CallCtx();
     if (!c) return fail(VR_ERROR_OUT_OF_MEMORY, "call context allocation failed");
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    // blocking sync: a host-buffer call waits on `done` asleep, not spinning a core (8 spinning
+    // callers under a 16-CPU quota throttled the whole process for ~10 ms at a time)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming | hipEventBlockingSync);
     if (e == hipSuccess) e = hipMalloc(&c->queue, 256);
     if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, 256, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1344,12 +1482,20 @@ int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation
     double *state = nullptr, *planar = nullptr;
     rc = host_call_scratch(c, n, 0, &state, &planar, nullptr);
     if (rc) return rc;
+    // one sample into a fresh buffer (vr_partial_render_scene, the reference's per-call pattern):
+    // only colour_sum comes back (24 B per pixel), the host derives the other four arrays
+    const bool fresh1 = !p->accumulate && p->spp == 1;
+    const size_t payload = (fresh1 ? 24 : 88) * n;
+    rc = ctx_grow_pinned(c, payload + 256);  // + the call's error word
+    if (rc) return rc;
+    double* host = (double*)c->pinned;  // same layout as `planar`
     const size_t b3 = n * 3 * sizeof(double), b1 = n * sizeof(double);
     if (p->accumulate) {  // continue update_pixel from the caller's buffer
-        VR_HIP(hipMemcpyAsync(planar + 3 * n, buf->colour_sum, b3, hipMemcpyHostToDevice, st));
-        VR_HIP(hipMemcpyAsync(planar + 6 * n, buf->colour_bias, b3, hipMemcpyHostToDevice, st));
-        VR_HIP(hipMemcpyAsync(planar + 9 * n, buf->weight, b1, hipMemcpyHostToDevice, st));
-        VR_HIP(hipMemcpyAsync(planar + 10 * n, buf->weight_bias, b1, hipMemcpyHostToDevice, st));
+        parallel_copy(host + 3 * n, buf->colour_sum, b3);
+        parallel_copy(host + 6 * n, buf->colour_bias, b3);
+        parallel_copy(host + 9 * n, buf->weight, b1);
+        parallel_copy(host + 10 * n, buf->weight_bias, b1);
+        VR_HIP(hipMemcpyAsync(planar + 3 * n, host + 3 * n, 2 * b3 + 2 * b1, hipMemcpyHostToDevice, st));
         const int e = vr::launch_buffer_convert(planar, state, n, 0, st);
         if (e) return fail(VR_ERROR_DEVICE, std::string("buffer import: ") + hipGetErrorString((hipError_t)e));
     } else {  // AccumulationBuffer::new
@@ -1357,15 +1503,56 @@ int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation
     }
     rc = enqueue_passes(ms, c, p, state, st, c->error, false, false, nullptr, nullptr, nullptr);
     if (rc) return rc;
-    const int e = vr::launch_buffer_convert(state, planar, n, 1, st);
+    const int e = vr::launch_buffer_convert(state, planar, n, fresh1 ? 2 : 1, st);
     if (e) return fail(VR_ERROR_DEVICE, std::string("buffer export: ") + hipGetErrorString((hipError_t)e));
-    VR_HIP(hipMemcpyAsync(buf->colour, planar, b3, hipMemcpyDeviceToHost, st));
-    VR_HIP(hipMemcpyAsync(buf->colour_sum, planar + 3 * n, b3, hipMemcpyDeviceToHost, st));
-    VR_HIP(hipMemcpyAsync(buf->colour_bias, planar + 6 * n, b3, hipMemcpyDeviceToHost, st));
-    VR_HIP(hipMemcpyAsync(buf->weight, planar + 9 * n, b1, hipMemcpyDeviceToHost, st));
-    VR_HIP(hipMemcpyAsync(buf->weight_bias, planar + 10 * n, b1, hipMemcpyDeviceToHost, st));
+    VR_HIP(hipMemcpyAsync(host, planar, fresh1 ? b3 : 3 * b3 + 2 * b1, hipMemcpyDeviceToHost, st));
+    volatile int32_t* flag = (volatile int32_t*)((char*)host + payload);  // the error word rides along
+    VR_HIP(hipMemcpyAsync((void*)flag, c->error, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     VR_HIP(hipEventRecord(c->done, st));
-    return read_and_clear_error(c->error, st);  // synchronises the call's stream
+    static const bool host_timing = getenv("VR_HOST_TIMING") != nullptr;  // diagnostic (tools/dropin.py)
+    const auto t_enq = std::chrono::steady_clock::now();
+    VR_HIP(hipEventSynchronize(c->done));
+    if (*flag) {
+        VR_HIP(hipMemsetAsync(c->error, 0, sizeof(int32_t), st));
+        VR_HIP(hipStreamSynchronize(st));
+        return fail(VR_ERROR_SINGULAR_BASIS,
+                    "Normal, tangent and cotangent don't form a valid basis (det == 0); the reference panics here");
+    }
+    const auto t_dev = std::chrono::steady_clock::now();
+    struct Report {
+        bool on;
+        std::chrono::steady_clock::time_point a, b;
+        ~Report() {
+            if (on)
+                std::fprintf(stderr, "vr_render_tile host timing: device wait %.3f ms, host copy-out %.3f ms\n",
+                             std::chrono::duration<double, std::milli>(b - a).count(),
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b).count());
+        }
+    } report{host_timing, t_enq, t_dev};
+    if (fresh1) {
+        // update_pixel (accumulation_buffer.rs:44-60) from zeros with weight 1: weight 1, weight bias
+        // (1 - 0) - 1 = 0; colour_sum t = 0 + y with y = c * 1 - 0, so y == t bit for bit except y = -0
+        // (t = +0), where the bias (t - 0) - y is +0 either way; colour = t * (1 / 1)
+        parallel_range(n, (uint64_t)1 << 14, [&](uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; ++i) {
+                for (int k = 0; k < 3; ++k) {
+                    const double t = host[3 * i + k];
+                    buf->colour_sum[3 * i + k] = t;
+                    buf->colour_bias[3 * i + k] = (t - 0.0) - t;
+                    buf->colour[3 * i + k] = t * (1.0 / 1.0);
+                }
+                buf->weight[i] = 1.0;
+                buf->weight_bias[i] = 0.0;
+            }
+        });
+    } else {
+        parallel_copy(buf->colour, host, b3);
+        parallel_copy(buf->colour_sum, host + 3 * n, b3);
+        parallel_copy(buf->colour_bias, host + 6 * n, b3);
+        parallel_copy(buf->weight, host + 9 * n, b1);
+        parallel_copy(buf->weight_bias, host + 10 * n, b1);
+    }
+    return VR_OK;
 }
 
 int vr_partial_render_scene(const vr_scene* s, vr_tile tile, uint64_t height, uint64_t width,
@@ -1454,16 +1641,22 @@ int vr_merge_tile(vr_accumulation_buffer* dst, vr_tile t, const vr_accumulation_
         t.end_row > dst->height || src->width != t.end_column - t.start_column ||
         src->height != t.end_row - t.start_row)
         return fail(VR_ERROR_INVALID_ARGUMENT, "merge_tile: tile does not match the buffers");
-    for (uint64_t i = 0; i < src->height; ++i) {
-        for (uint64_t j = 0; j < src->width; ++j) {
-            const uint64_t d = (t.start_row + i) * dst->width + (t.start_column + j), q = i * src->width + j;
-            const double w1 = dst->weight[d], w2 = src->weight[q];
-            const double inv = 1.0 / (w1 + w2);
-            for (int k = 0; k < 3; ++k)
-                dst->colour[3 * d + k] = (dst->colour[3 * d + k] * w1 + src->colour[3 * q + k] * w2) * inv;
-            dst->weight[d] = w1 + w2;
+    // blend (accumulation_buffer.rs:87-91) per pixel; rows are independent, so a large tile is
+    // split into row bands over host threads (96 B of memory traffic per pixel: one core merged
+    // a 1024^2 frame in ~5 ms, the bottleneck of main.rs's one merging thread)
+    auto rows = [&](uint64_t r0, uint64_t r1) {
+        for (uint64_t i = r0; i < r1; ++i) {
+            for (uint64_t j = 0; j < src->width; ++j) {
+                const uint64_t d = (t.start_row + i) * dst->width + (t.start_column + j), q = i * src->width + j;
+                const double w1 = dst->weight[d], w2 = src->weight[q];
+                const double inv = 1.0 / (w1 + w2);
+                for (int k = 0; k < 3; ++k)
+                    dst->colour[3 * d + k] = (dst->colour[3 * d + k] * w1 + src->colour[3 * q + k] * w2) * inv;
+                dst->weight[d] = w1 + w2;
+            }
         }
-    }
+    };
+    parallel_range(src->height, std::max<uint64_t>(1, ((uint64_t)1 << 16) / std::max<uint64_t>(1, src->width)), rows);
     return VR_OK;
 }
 

@@ -88,6 +88,16 @@ __global__ __launch_bounds__(256) void export_buffer_kernel(const double* __rest
     planar[9 * npix + p] = w;
     planar[10 * npix + p] = r[7];
 }
+// A fresh buffer after exactly one sample per pixel (vr_partial_render_scene): weight 1, weight
+// bias 0, and colour / colour_bias follow from colour_sum alone, so only the sums cross PCIe
+// (24 of the 88 B per pixel); the host expands them (vr_host.cpp expand_fresh_one_sample).
+__global__ __launch_bounds__(256) void export_sums_kernel(const double* __restrict__ state, uint64_t npix,
+                                                          double* __restrict__ sums) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    const double* r = state + p * 8;
+    for (int k = 0; k < 3; ++k) sums[3 * p + k] = r[k];
+}
 __global__ __launch_bounds__(256) void import_buffer_kernel(const double* __restrict__ planar, uint64_t npix,
                                                             double* __restrict__ state) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -105,7 +115,8 @@ __global__ __launch_bounds__(256) void import_buffer_kernel(const double* __rest
 int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_planar, void* stream) {
     if (npix == 0) return 0;
     const dim3 grid((unsigned)((npix + 255) / 256)), block(256);
-    if (to_planar) hipLaunchKernelGGL(dev::export_buffer_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
+    if (to_planar == 2) hipLaunchKernelGGL(dev::export_sums_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
+    else if (to_planar) hipLaunchKernelGGL(dev::export_buffer_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
     else hipLaunchKernelGGL(dev::import_buffer_kernel, grid, block, 0, (hipStream_t)stream, src, npix, dst);
     return (int)hipGetLastError();
 }

@@ -180,7 +180,8 @@ int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool r
 // vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
 // vr_image.hip: device records (8 f64 per pixel) <-> the host AccumulationBuffer's five arrays laid
-// out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read)
+// out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read;
+// 2: records -> colour_sum only, 3 f64 per pixel)
 int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_planar, void* stream);
 // vr_build.hip: one mesh's BVH on the device (same nodes and leaf order as the host build)
 int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,

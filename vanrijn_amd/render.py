@@ -78,6 +78,18 @@ class AccumulationBuffer:
     def new(width, height):
         return AccumulationBuffer(width, height)
 
+    @classmethod
+    def _for_output(cls, width, height):
+        """A buffer the library overwrites completely (all five arrays): allocated without the
+        zeroing pass, which cost as much host time as the render itself at 1 spp."""
+        b = cls.__new__(cls)
+        b.colour_buffer = np.empty((height, width, 3))
+        b.colour_sum_buffer = np.empty((height, width, 3))
+        b.colour_bias_buffer = np.empty((height, width, 3))
+        b.weight_buffer = np.empty((height, width))
+        b.weight_bias_buffer = np.empty((height, width))
+        return b
+
     def width(self):
         return self.colour_buffer.shape[1]
 
@@ -138,7 +150,7 @@ def _params(tile, height, width, spp, seed, first_sample, accumulate):
 def partial_render_scene(scene, tile: Tile, height: int, width: int, device=0) -> AccumulationBuffer:
     """camera.rs:95-130: one sample per pixel of `tile` into a fresh tile AccumulationBuffer."""
     ds = _scene_handle(scene, device)
-    out = AccumulationBuffer(tile.width(), tile.height())
+    out = AccumulationBuffer._for_output(tile.width(), tile.height())
     oc = out._c()
     N.check(N.lib().vr_partial_render_scene(ds.handle, tile._c(), height, width, C.byref(oc)))
     return out
@@ -148,7 +160,7 @@ def render_tile(scene, tile: Tile, height, width, spp, seed, first_sample=0, acc
                 device=0) -> AccumulationBuffer:
     """spp samples per pixel with explicit seed / sample range (update_pixel semantics)."""
     ds = _scene_handle(scene, device)
-    buf = accumulate if accumulate is not None else AccumulationBuffer(tile.width(), tile.height())
+    buf = accumulate if accumulate is not None else AccumulationBuffer._for_output(tile.width(), tile.height())
     bc = buf._c()
     p = _params(tile, height, width, spp, seed, first_sample, accumulate is not None)
     N.check(N.lib().vr_render_tile(ds.handle, C.byref(p), C.byref(bc)))
