@@ -58,11 +58,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 struct Rng {
-    uint64_t base;
-    uint64_t k;
+    uint64_t cur;  // base + k * kGolden after k draws: draw k + 1 adds kGolden (no 64-bit multiply)
+    __device__ __forceinline__ void reset(uint64_t base) { cur = base; }
     __device__ __forceinline__ uint64_t next() {
-        k += 1;
-        return mix64(base + k * kGolden);
+        cur += kGolden;
+        return mix64(cur);
     }
     // rand 0.7 Standard f64 (camera.rs:49, photon.rs:21)
     __device__ __forceinline__ double standard() { return (double)(next() >> 11) * 0x1.0p-53; }
@@ -78,6 +78,10 @@ __device__ __forceinline__ uint64_t stream_base(uint64_t seed, uint64_t pixel, u
     uint64_t k = mix64(seed ^ kSeedSalt);
     k = mix64(k + pixel);
     return mix64(k + sample);
+}
+// the same, from seed_key = mix64(seed ^ kSeedSalt) (a per-launch constant, RenderArgs::seed_key)
+__device__ __forceinline__ uint64_t stream_base_keyed(uint64_t seed_key, uint64_t pixel, uint64_t sample) {
+    return mix64(mix64(seed_key + pixel) + sample);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -321,6 +325,22 @@ __device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo
     if (hi - lo > 2.0f * e) return 1;
     if (lo - hi > 2.0f * e) return 0;
     return 2;
+}
+// slab32 as two flags (the node step's form, no integer result to re-test): `maybe` = the exact
+// test may pass (slab32 != 0), `sure` = it certainly passes (slab32 == 1)
+__device__ __forceinline__ void slab32_flags(const float* b, const Ray32& r, float& tlo, float& thi, bool& maybe,
+                                             bool& sure) {
+    const vr_f2 bx = {b[0], b[1]}, by = {b[2], b[3]}, bz = {b[4], b[5]};
+    const vr_f2 tx = __builtin_elementwise_fma(bx, (vr_f2){r.ix, r.ix}, (vr_f2){r.nx, r.nx});
+    const vr_f2 ty = __builtin_elementwise_fma(by, (vr_f2){r.iy, r.iy}, (vr_f2){r.ny, r.ny});
+    const vr_f2 tz = __builtin_elementwise_fma(bz, (vr_f2){r.iz, r.iz}, (vr_f2){r.nz, r.nz});
+    const float lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    const float hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    const float e = r.ek + 3e-7f * (fabsf(lo) + fabsf(hi));
+    tlo = lo - e;
+    thi = hi + e;
+    sure = hi - lo > 2.0f * e;
+    maybe = sure || !(lo - hi > 2.0f * e);
 }
 
 // A triangle record in one batch of five dwordx4 loads.  Left to itself the scheduler issued the

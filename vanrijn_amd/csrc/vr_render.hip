@@ -84,6 +84,16 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
 #define VR_PEND 8
 #endif
 constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
+// Wave-level leaf queue (VR_WAVE_LEAF, default): the leaf triangles a wave's lanes meet go to one
+// FIFO per wave, tagged with the lane whose ray met them, and a leaf round hands the oldest 64 to
+// the 64 lanes -- each tests one against its owner's ray (fetched by cross-lane permute), and the
+// owners merge their results through LDS atomics.  The f64 triangle test then runs with every
+// lane busy; with per-lane queues a round tested one triangle per lane that had one (17 of 64).
+#ifndef VR_WAVE_LEAF
+#define VR_WAVE_LEAF 1
+#endif
+constexpr int kWaveList = 64 * kPend;  // FIFO entries per wave: each lane owns at most kPend
+static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
 
 // The kernel argument block, re-read through a pointer the compiler cannot prove unchanged: the
 // tree and triangle base pointers become scalar loads at their use.  Held in SGPRs for the whole
@@ -114,15 +124,37 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // leaf triangles met during traversal wait here for a leaf round, in which every lane with
     // one tests it: the f64 triangle test then runs for many lanes at once instead of for the few
     // that reached a leaf in this step.  [slot][thread], LIFO, kPend slots per lane.
+#if VR_WAVE_LEAF
+    // per wave: the FIFO of queued leaves (triangle | exact-box flag, and the owning lane) and, per
+    // owner lane, one leaf round's results: entries tested, min distance bits, max rank at that
+    // distance, and that triangle
+    __shared__ int32_t wl_tri[4 * kWaveList];
+    __shared__ uint8_t wl_own[4 * kWaveList];
+    __shared__ unsigned long long lr_d[256];
+    __shared__ uint32_t lr_rank[256], lr_tri[256], lr_cnt[256];
+    const int wbase = (threadIdx.x >> 6) * kWaveList;
+    uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
+#else
     __shared__ int32_t st_pend[kPend * 256];
+#endif
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
+#if VR_WAVE_LEAF
+    lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
+    lr_rank[tid] = 0;
+    lr_cnt[tid] = 0;
+#endif
     DeviceScene S = A.scene;
     S.prims = g_prims;
     S.materials = g_materials;
     S.bvhs = g_bvhs;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t sec[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef VR_MARKS  // ISA section markers for tools/isa_sections.py (analysis builds only)
+#define VR_MARK(name) asm volatile(";@mark " name)
+#else
+#define VR_MARK(name)
+#endif
 #define VR_SEC(i) \
     if (COUNT && first_active_lane()) sec[i]++;
     uint64_t cyc[6] = {0, 0, 0, 0, 0, 0}, tprev = COUNT ? __builtin_amdgcn_s_memtime() : 0;
@@ -145,13 +177,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     uint32_t s_idx = 0;
     uint64_t w_next = 0, w_end = 0;  // this wave's slice of the queue (grab > 0)
     Rng rng;
-    rng.base = 0;
-    rng.k = 0;
+    rng.reset(0);
     RayPre pre;
     Ray32 pre32;
     Best best;
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
-    int np = 0;  // pending leaf triangles in st_pend
+    int np = 0;  // this lane's queued leaf triangles not yet tested
     // f32 forms of the cull thresholds: cull_far >= bound + margin (rounded up), cull_behind <=
     // -behind_margin (rounded down; -inf when behind-culling is off) -- never tighter than f64
     float cull_far = INFINITY, cull_behind = -INFINITY;
@@ -181,6 +212,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         const TriVerts tv = load_tri(VR_TRIS + tri);
         if (e < 0) {
             VR_SEC(2);
+            VR_MARK("exact_box");
             if (COUNT) cnt.exact_boxes++;
             double bb[6], lo, hi;
 #pragma unroll
@@ -207,6 +239,93 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             set_cull_far();
         }
     };
+#if VR_WAVE_LEAF
+    // One leaf round over the n (<= 64) oldest entries of the wave FIFO: lane i tests entry i
+    // against its owner's ray.  Per owner, the round's candidate is the minimum distance and, among
+    // equal distances, the highest reference rank (LDS atomics; one wave's LDS operations execute
+    // in order): applied to `best` with test_tri's rule it gives what testing the entries one by
+    // one in any order gives (closest_intersection keeps the later leaf on ties, sampler.rs keeps
+    // the earlier object).  Called with the whole wave active.
+    auto leaf_round = [&](uint32_t n) {
+        const bool mine = lane < n;
+        int e = 0;
+        uint32_t owner = lane;
+        if (mine) {
+            const uint32_t pos = (q_head + lane) & (kWaveList - 1);
+            e = wl_tri[wbase + pos];
+            owner = wl_own[wbase + pos];
+        }
+        RayPre op;  // the owner's ray
+        op.o.x = __shfl(pre.o.x, (int)owner);
+        op.o.y = __shfl(pre.o.y, (int)owner);
+        op.o.z = __shfl(pre.o.z, (int)owner);
+        op.d.x = __shfl(pre.d.x, (int)owner);
+        op.d.y = __shfl(pre.d.y, (int)owner);
+        op.d.z = __shfl(pre.d.z, (int)owner);
+        op.sx = __shfl(pre.sx, (int)owner);
+        op.sy = __shfl(pre.sy, (int)owner);
+        op.pdz = __shfl(pre.pdz, (int)owner);
+        op.flags = __shfl(pre.flags, (int)owner);
+        const int oslot = (tid & ~63) + (int)owner;
+        double d = -1.0;
+        uint32_t rank = 0;
+        const int tri = e & 0x7fffffff;
+        if (mine) {
+            const TriVerts tv = load_tri(VR_TRIS + tri);
+            bool reach = true;
+            if (e < 0) {  // the leaf's f32 box test was too close to call: the exact one decides
+                VR_SEC(2);
+                VR_MARK("exact_box");
+                if (COUNT) cnt.exact_boxes++;
+                double bb[6], lo, hi;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    bb[2 * a] = fmin(fmin(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                    bb[2 * a + 1] = fmax(fmax(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                }
+                reach = slab(bb, op, lo, hi);
+            }
+            if (reach) {
+                if (COUNT) cnt.tri_tests++;
+                double b[3];
+                d = triangle_distance(tv, op, b);
+                rank = (uint32_t)tv.rank;
+            }
+            atomicAdd(&lr_cnt[oslot], 1u);
+        }
+        const bool hit = mine && d >= 0.0;
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+        if (hit) atomicMin(&lr_d[oslot], bits);
+        const bool at_min = hit && lr_d[oslot] == bits;
+        if (at_min) atomicMax(&lr_rank[oslot], rank);
+        if (at_min && lr_rank[oslot] == rank) lr_tri[oslot] = (uint32_t)tri;
+        // owners: fold the round's candidate into the closest hit
+        const uint32_t got = lr_cnt[tid];
+        if (got) {
+            np -= (int)got;
+            const unsigned long long db = lr_d[tid];
+            if (db != ~0ull) {
+                const double dd = __longlong_as_double((long long)db);
+                const uint32_t rk = lr_rank[tid];
+                bool take;
+                if (!best.kind || dd < best.d) take = true;
+                else if (dd == best.d)
+                    take = (best.object == cur_object) ? ((int64_t)rk > S.tris[best.index].rank) : (cur_object < best.object);
+                else take = false;
+                if (take) {
+                    best.d = dd;
+                    best.kind = kTri;
+                    best.index = (int)lr_tri[tid];
+                    best.object = cur_object;
+                    set_cull_far();
+                }
+            }
+            lr_cnt[tid] = 0;
+            lr_d[tid] = ~0ull;
+            lr_rank[tid] = 0;
+        }
+    };
+#endif
     // next BVH (from bvh_i) with work; false when the ray is fully traced
     auto start_bvhs = [&]() {
         for (; bvh_i < S.bvh_count; ++bvh_i) {
@@ -280,6 +399,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // (ColourXyz::from_photon of photon.scale_intensity(360)) and the Kahan sums
     auto finish = [&](double wl, double I) {
         VR_SEC(6);
+        VR_MARK("finish");
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
         // streamed once to HBM and read once by the reduce: non-temporal, so the 16 B per sample
         // (4.3 GB per 1024^2 x 256 frame) do not evict the BVH and triangles from L2 and MALL
@@ -306,6 +426,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // closest hit, forward form: returns true when a bounce ray was started
     auto shade = [&]() {
         VR_SEC(3);
+        VR_MARK("shade");
         HitInfo h;
         hit_info(S, best, pre, h);
         if (COUNT && best.kind == kTri) cnt.shaded++;
@@ -474,9 +595,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
         // that only meet the plane or spheres), so those lanes do not idle through phase B
         for (int rep = 0; rep < A.phase_a_reps; ++rep) {
+            VR_MARK("phaseA_top");
             if (COUNT && first_active_lane()) cnt.outer_slots += 64;
             VR_STAMP(5);
             if (state == kTraversed) {
+                VR_MARK("traversed");
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
                 bool go = false;
@@ -513,12 +636,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 if (go) shade();
             }
             VR_STAMP(0);
+            VR_MARK("refill_check");
             // refill: lanes whose item is exhausted take the next items (one atomic per wave)
             while (true) {
                 const bool need = state == kNeedRay && s_idx >= s_end;
                 const uint64_t m = __ballot(need);
                 if (m == 0) break;
                 VR_SEC(7);
+                VR_MARK("refill");
                 const unsigned leader = (unsigned)__builtin_ctzll(m);
                 const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
                 unsigned long long base = 0;
@@ -575,10 +700,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             VR_STAMP(1);
             if (state == kNeedRay) {
                 const uint64_t row = A.start_row + py, col = A.start_column + px;
-                rng.base = stream_base(A.seed, row * A.width + col, A.first_sample + s_idx);
-                rng.k = 0;
+                rng.reset(stream_base_keyed(A.seed_key, row * A.width + col, A.first_sample + s_idx));
                 // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
                 VR_SEC(4);
+                VR_MARK("camera");
                 // film_w * (1 / w), film_w * 0.5, ... are per-launch constants (host: make_args)
                 const double ux = rng.standard();
                 const double uy = rng.standard();
@@ -593,6 +718,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             if (state == kRayReady) {
                 VR_SEC(5);
+                VR_MARK("begin_ray");
                 begin_ray();
             }
             VR_STAMP(2);
@@ -604,8 +730,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         do {
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             VR_STAMP(5);
+            VR_MARK("phaseB_top");
             // node step (4-wide node): lanes with room for four more pending leaves
+#if VR_WAVE_LEAF
+            uint32_t lmask = 0;  // leaf children this lane queues in this step
+            int32_t lent[4];
+#endif
             if (state == kTraversing && node >= 0 && np <= kPend - 4) {
+                VR_MARK("node_step");
                 const Node4& nd = VR_NODES4[node];
                 if (COUNT) cnt.node_visits++;
                 int c[4];
@@ -621,22 +753,29 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 for (int k = 0; k < 4; ++k) {
                     c[k] = nd.child[k];
                     float g;
-                    const int r = slab32(nd.box[k], pre32, f[k], g);
+                    bool maybe, sure;
+                    slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
                     const bool live = c[k] != kEmptyChild;
                     if (COUNT && live) cnt.box_tests++;
-                    const bool pass = live && r != 0 && !(f[k] > cull_far || g < cull_behind);
+                    const bool pass = live && maybe && !(f[k] > cull_far || g < cull_behind);
                     hm |= pass ? 1u << k : 0u;
-                    xm |= (pass && r == 2) ? 1u << k : 0u;
+                    xm |= (pass && !sure) ? 1u << k : 0u;
                 }
-                // leaf children: queue their triangles (unconditional LDS writes, the count
-                // advances only for hits; np <= kPend - 4 leaves room for all four)
+                // leaf children: queue their triangles (per-lane queue: unconditional LDS writes,
+                // the count advances only for hits; np <= kPend - 4 leaves room for all four;
+                // wave queue: appended after the step, by all lanes at once)
                 float key[4];
                 int ch[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const bool h = (hm >> k) & 1u;
+#if VR_WAVE_LEAF
+                    lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
+                    lmask |= (h && c[k] < 0) ? 1u << k : 0u;
+#else
                     st_pend[np * 256 + tid] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
                     np += (h && c[k] < 0) ? 1 : 0;
+#endif
                     // hit: a finite key (NaN or infinite f32 bounds of exactly-decided children
                     // clamp into range); INFINITY marks "not descended"
                     key[k] = (h && c[k] >= 0) ? fminf(fmaxf(f[k], -FLT_MAX), FLT_MAX) : INFINITY;
@@ -675,6 +814,36 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
             }
             VR_STAMP(3);
+            VR_MARK("leaf_check");
+#if VR_WAVE_LEAF
+            // append this step's leaves to the wave FIFO in (child slot, lane) order
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool lh = (lmask >> k) & 1u;
+                const uint64_t m = __ballot(lh);
+                if (lh) {
+                    const uint32_t pos = (q_tail + (uint32_t)__popcll(m & ((1ull << lane) - 1))) & (kWaveList - 1);
+                    wl_tri[wbase + pos] = lent[k];
+                    wl_own[wbase + pos] = (uint8_t)lane;
+                }
+                q_tail += (uint32_t)__popcll(m);
+                np += lh ? 1 : 0;
+            }
+            q_tail = __builtin_amdgcn_readfirstlane(q_tail);
+            // leaf round: 64 queued leaves (every lane busy), or enough lanes (or all) are stalled
+            // on theirs
+            const uint32_t queued = q_tail - q_head;
+            if (queued != 0) {
+                const bool stalled = np > 0 && (node < 0 || np > kPend - 4);
+                if (queued >= 64 || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
+                    __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
+                    VR_SEC(0);
+                    VR_MARK("leaf_test");
+                    leaf_round(queued < 64u ? queued : 64u);
+                    q_head = __builtin_amdgcn_readfirstlane(q_head + (queued < 64u ? queued : 64u));
+                }
+            }
+#else
             // leaf round: enough lanes have a pending triangle, or enough lanes (or all) are
             // stalled on theirs
             const uint64_t pm = __ballot(np > 0);
@@ -685,14 +854,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
                     if (np > 0) {
                         VR_SEC(0);
+                        VR_MARK("leaf_test");
                         --np;
                         test_tri(st_pend[np * 256 + tid]);
                     }
                 }
             }
+#endif
             VR_STAMP(4);
             if (state == kTraversing && node < 0 && np == 0) {
                 VR_SEC(8);
+                VR_MARK("next_bvh");
                 ++bvh_i;
                 if (!start_bvhs()) state = kTraversed;
             }
