@@ -590,6 +590,15 @@ static void parallel_copy(void* dst, const void* src, size_t bytes) {
     });
 }
 
+// spectrum.rs:64-79's sample wavelengths as the reference computes them (before / after), and the
+// reciprocal step for the device's segment index (intensity only: a neighbouring segment at a knot
+// gives the same value to rounding)
+static void fill_knots(vr::Material& m) {
+    const double range = m.longest - m.shortest;
+    for (int j = 0; j < m.n; ++j) m.knots[j] = (double)j / (double)(m.n - 1) * range + m.shortest;
+    m.inv_step = m.n > 1 && range > 0.0 ? (double)(m.n - 1) / range : 0.0;
+}
+
 namespace {
 
 int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }  // binary tree walks
@@ -1007,6 +1016,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         dm.reflection = m.reflection_strength;
         dm.smoothness = m.smoothness;
         std::memcpy(dm.samples, m.colour.samples, sizeof(double) * m.colour.sample_count);
+        fill_knots(dm);
         s->materials.push_back(dm);
         if (vr_spectrum_intensity_at_wavelength(&m.colour, 0.0) != 0.0) s->dark0 = false;
         s->mats |= m.kind == VR_MATERIAL_LAMBERTIAN ? 1 : (m.kind == VR_MATERIAL_REFLECTIVE ? 2 : 4);
@@ -1025,6 +1035,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
             dm.shortest = sp.shortest_wavelength;
             dm.longest = sp.longest_wavelength;
             std::memcpy(dm.samples, sp.samples, sizeof(double) * sp.sample_count);
+            fill_knots(dm);
             return true;
         };
         s->dev.integrator = VR_INTEGRATOR_WHITTED;
@@ -1041,6 +1052,15 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         }
     } else if (desc->integrator && desc->integrator->kind != VR_INTEGRATOR_SIMPLE_RANDOM) {
         return bad("unknown integrator kind");
+    }
+    {  // the sky's lookup row (test_lighting_environment's RGB-basis spectrum: 32 samples)
+        vr::Material sky{};
+        sky.n = 32;
+        sky.shortest = VR_RGBSPEC_SHORTEST;
+        sky.longest = VR_RGBSPEC_LONGEST;
+        fill_knots(sky);
+        s->dev.sky_row = (int32_t)s->materials.size();
+        s->materials.push_back(sky);
     }
     // objects: primitive lists keep their order; BVHs are built per mesh
     std::vector<int> mesh_object(desc->mesh_count, -1);
@@ -1068,9 +1088,14 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
                     dp.vec[0] = n.x; dp.vec[1] = n.y; dp.vec[2] = n.z;
                     dp.tan[0] = tan.x; dp.tan[1] = tan.y; dp.tan[2] = tan.z;
                     dp.cot[0] = cot.x; dp.cot[1] = cot.y; dp.cot[2] = cot.z;
+                    dp.pre[0] = n.x * p.scalar; dp.pre[1] = n.y * p.scalar; dp.pre[2] = n.z * p.scalar;
                     extent = std::max(extent, std::fabs(p.scalar));
                 } else if (p.kind == VR_PRIMITIVE_SPHERE) {
                     dp.vec[0] = p.vector.x; dp.vec[1] = p.vector.y; dp.vec[2] = p.vector.z;
+                    dp.pre[0] = p.vector.x * p.vector.x;
+                    dp.pre[1] = p.vector.y * p.vector.y;
+                    dp.pre[2] = p.vector.z * p.vector.z;
+                    dp.scalar2 = p.scalar * p.scalar;
                     extent = std::max({extent, std::fabs(p.vector.x) + std::fabs(p.scalar),
                                        std::fabs(p.vector.y) + std::fabs(p.scalar),
                                        std::fabs(p.vector.z) + std::fabs(p.scalar)});

@@ -67,6 +67,11 @@ struct Material {
     double diffuse, reflection;  // reflection = Phong's specular_strength
     double smoothness;           // Phong exponent
     double samples[kMaxSpectrumSamples];
+    // spectrum.rs:64-79's sample wavelengths, (j / (n - 1)) * range + shortest, evaluated on the
+    // host with the reference's operations (bit-identical), and (n - 1) / range: the device's
+    // intensity lookup (material_intensity) needs one division instead of four
+    double knots[kMaxSpectrumSamples];
+    double inv_step;
 };
 
 // Plane (after Plane::new) or sphere.
@@ -79,6 +84,11 @@ struct Prim {
     double tan[3];     // plane tangent
     double cot[3];     // plane cotangent
     double scalar;     // plane distance / sphere radius
+    // ray-independent products the tests would recompute per ray (same f64 operations, so the
+    // same bits): plane: q = normal * distance (plane.rs:57); sphere: centre * centre per
+    // component and radius * radius (sphere.rs:48-57)
+    double pre[3];
+    double scalar2;
 };
 
 struct Bvh {
@@ -113,7 +123,7 @@ struct DeviceScene {
     int32_t integrator;
     int32_t light_count;
     int32_t light_base;
-    int32_t pad_i;
+    int32_t sky_row;       // materials[sky_row]: knots / inv_step of the RGB basis (the sky lookup)
     const double* light_dirs;
 };
 

@@ -455,10 +455,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const RayPre sp = prepare(Ray{add(h.loc, scl(d1, kBounceBias)), normalize(d1)});
                 double term;
                 if (any_hit<STACK>(S, sp, st_node, tid)) {
-                    term = material_colour(&S.materials[S.light_base], lambda);
+                    term = material_intensity(&S.materials[S.light_base], lambda);
                 } else {
                     const V3 wl = mk(dot(h.tangent, ldir), dot(h.cotangent, ldir), dot(h.normal, ldir));
-                    const double I = material_colour(&S.materials[S.light_base + 1 + j], lambda) * fabs(dot(ldir, h.normal));
+                    const double I = material_intensity(&S.materials[S.light_base + 1 + j], lambda) * fabs(dot(ldir, h.normal));
                     double ba, bb;
                     bsdf_affine(mat, w_i, wl, lambda, ba, bb);
                     term = ba * I + bb;
@@ -534,8 +534,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             state = kRayReady;
             return;
         }
-        const double c_l = material_colour(mat, lambda);
-        const double c_0 = DARK0 ? 0.0 : material_colour(mat, 0.0);
+        const double c_l = material_intensity(mat, lambda);
+        const double c_0 = DARK0 ? 0.0 : material_intensity(mat, 0.0);
         double a, a0, bterm;
         if (kind == 1) {  // reflective_material.rs:17-39
             if (w_i.z <= 0.0 || w_o.z <= 0.0) {
@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         go = true;
                     }
                 } else if (!best.kind) {
-                    finish(lambda, Acc + T * sky_intensity(wo_y, lambda));  // simple_random_integrator.rs:43-46
+                    finish(lambda, Acc + T * sky_intensity(wo_y, lambda, &S.materials[S.sky_row]));  // simple_random_integrator.rs:43-46
                 } else {
                     depth += 1;
                     if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
