@@ -25,7 +25,10 @@ d = collections.defaultdict(list)
 for line in open("gpurun_out/ab_libs.jsonl"):
     name, js = line.split(" ", 1)
     r = json.loads(js)
-    d[(r["scene"], name)].append(r["median_ms"])
+    d[(r["scene"], name)].append((r["median_ms"], r.get("reduce_ms", 0.0)))
 for k, v in sorted(d.items()):
-    print(k, "median of medians %.3f ms" % sorted(v)[len(v) // 2], ["%.2f" % x for x in v])
+    ms = sorted(x[0] for x in v)
+    red = sorted(x[1] for x in v)
+    print(k, "median of medians %.3f ms (reduce %.3f ms)" % (ms[len(ms) // 2], red[len(red) // 2]),
+          ["%.2f" % x[0] for x in v])
 PY

@@ -51,11 +51,12 @@ def main():
             if ref is None:
                 ref = out
             same = bool(torch.equal(out, ref))
-            results.setdefault((v, t, e), []).append((st["kernel_ms"], same))
+            results.setdefault((v, t, e), []).append((st["kernel_ms"], same, st.get("reduce_ms", 0.0)))
     for (v, t, e), r in results.items():
         ms = [x[0] for x in r]
         print(json.dumps({"variant": v, "threshold": t, **dict(zip(names, e)), "scene": a.scene,
                           "median_ms": statistics.median(ms), "min_ms": min(ms),
+                          "reduce_ms": statistics.median([x[2] for x in r]),
                           "msamples_s": W * H * a.spp / statistics.median(ms) / 1e3,
                           "bitwise_equal_to_first": all(x[1] for x in r)}), flush=True)
 

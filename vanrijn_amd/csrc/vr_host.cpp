@@ -1366,8 +1366,11 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         }
         // LDS stack entries: the 4-wide walk's, and the binary walk's for Whitted shadow rays
         const int stack = s->dev.integrator == 1 ? std::max(stack_depth(s), wide_stack_depth(s)) : wide_stack_depth(s);
+        // persistent grid: 3 workgroups per CU (3 waves per SIMD); VR_GRID_PER_CU overrides
+        // (diagnostic: throughput against occupancy)
+        static const int per_cu = getenv("VR_GRID_PER_CU") ? std::max(1, atoi(getenv("VR_GRID_PER_CU"))) : 3;
         int lr = vr::launch_render(a, stack, counting, recording, s->dark0, s->mats ? s->mats : 3,
-                                   std::max(1, s->cu_count) * 3, st, mid);
+                                   std::max(1, s->cu_count) * per_cu, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {
             hipEvent_t end = timing->add();

@@ -794,8 +794,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 cas(0, 1);
                 cas(2, 3);
                 cas(0, 2);
+#ifndef VR_SORT_LIGHT  // experiment: nearest first, the other three only partly ordered
                 cas(1, 3);
                 cas(1, 2);
+#endif
                 if (key[0] < INFINITY) {
                     // farthest first, so the nearest remaining pops first (writes at sp are
                     // unconditional: the stack holds one spare entry)
@@ -830,12 +832,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 np += lh ? 1 : 0;
             }
             q_tail = __builtin_amdgcn_readfirstlane(q_tail);
-            // leaf round: 64 queued leaves (every lane busy), or enough lanes (or all) are stalled
-            // on theirs
+            // leaf round: leaf_threshold (64) queued leaves -- every lane busy --, or enough lanes (or
+            // all) are stalled on theirs
             const uint32_t queued = q_tail - q_head;
             if (queued != 0) {
                 const bool stalled = np > 0 && (node < 0 || np > kPend - 4);
-                if (queued >= 64 || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
+                if (queued >= A.leaf_threshold || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
                     __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
                     VR_SEC(0);
                     VR_MARK("leaf_test");
@@ -897,6 +899,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #undef VR_STAMP
 #undef VR_SEC
 
+typedef double d2 __attribute__((ext_vector_type(2)));
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
 __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const double* staging, uint64_t npix,
@@ -912,12 +915,8 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
         w = state[p * 8 + 6];
         wb = state[p * 8 + 7];
     }
-    for (uint32_t s = 0; s < spp; ++s) {
-        const double* ph = staging + ((uint64_t)s * npix + p) * 2;  // final photon {wavelength, intensity}
-        const double wl = __builtin_nontemporal_load(&ph[0]), I = __builtin_nontemporal_load(&ph[1]);
-        const double Is = I * 360.0;                                // photon.rs:26-28, camera.rs:121-126
-        const V3 cx = xyz_for_wavelength(wl);                       // colour_xyz.rs:31-35
-        const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
+    // update_pixel for one sample (the Kahan chain is sequential in s)
+    auto update = [&](const double c[3]) {
         const double wy = 1.0 - wb;
         const double wt = w + wy;
         wb = (wt - w) - wy;
@@ -929,6 +928,35 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
             bias[k] = (t - sum[k]) - y;
             sum[k] = t;
         }
+    };
+    // the colours of kB samples are independent (7 exp() each): computed together, then folded in
+    // order -- the same operations as one at a time, with kB-fold instruction-level parallelism
+    constexpr uint32_t kB = 4;
+    uint32_t s = 0;
+    for (; s + kB <= spp; s += kB) {
+        double c[kB][3];
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+            // final photon {wavelength, intensity}: one 16-B non-temporal load
+            const d2* ph = reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p);
+            const d2 v = __builtin_nontemporal_load(ph);
+            const double wl = v.x, I = v.y;
+            const double Is = I * 360.0;                // photon.rs:26-28, camera.rs:121-126
+            const V3 cx = xyz_for_wavelength_fast(wl);  // colour_xyz.rs:31-35
+            c[j][0] = cx.x * Is;
+            c[j][1] = cx.y * Is;
+            c[j][2] = cx.z * Is;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) update(c[j]);
+    }
+    for (; s < spp; ++s) {
+        const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)s * npix + p));
+        const double wl = v.x, I = v.y;
+        const double Is = I * 360.0;
+        const V3 cx = xyz_for_wavelength_fast(wl);
+        const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
+        update(c);
     }
     for (int k = 0; k < 3; ++k) {
         state[p * 8 + k] = sum[k];
