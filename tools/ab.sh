@@ -6,16 +6,15 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 R=${ROUNDS:-3}
 : > gpurun_out/ab_libs.jsonl
+SCENES=${SCENES:-"main:256 bench:32"}
+[ "${BENCH_SCENE:-1}" = 1 ] || SCENES="main:256"
 for r in $(seq 1 "$R"); do
   for L in "$@"; do
-    VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene main --spp 256 --reps 2 --variants 0 \
-        --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
-    rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
-    if [ "${BENCH_SCENE:-1}" = 1 ]; then
-      VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene bench --spp 32 --reps 2 --variants 0 \
+    for sc in $SCENES; do
+      VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene ${sc%%:*} --spp ${sc##*:} --reps 2 --variants 0 \
           --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
       rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
-    fi
+    done
   done
   echo "round $r done"
 done
