@@ -163,7 +163,14 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: run `python -m vanrijn_amd.build` (hipcc, gfx950) first")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                # an older build under A/B (tools/ab.sh, VR_LIBRARY) may predate a symbol; the
+                # in-tree library must export every one (tests/test_abi.py)
+                if os.environ.get("VR_LIBRARY"):
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         _lib = L
