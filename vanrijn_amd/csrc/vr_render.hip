@@ -106,7 +106,17 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
-constexpr int kWaveList = 64 * kPend;  // FIFO entries per wave: each lane owns at most kPend
+constexpr int kWaveList = 64 * kPend;
+// room for a node step's leaves: per lane (at most kPend queued per lane), or -- VR_WAVE_CAP --
+// for the wave (the FIFO has room for a step of all 64 lanes: any one lane may queue more)
+#ifndef VR_WAVE_CAP
+#define VR_WAVE_CAP 1
+#endif
+#if VR_WAVE_LEAF && VR_WAVE_CAP
+#define VR_ROOM (q_tail - q_head <= (uint32_t)(kWaveList - 256))
+#else
+#define VR_ROOM (np <= kPend - 4)
+#endif  // FIFO entries per wave: each lane owns at most kPend
 static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
 
 // The kernel argument block, re-read through a pointer the compiler cannot prove unchanged: the
@@ -752,7 +762,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             uint32_t lmask = 0;  // leaf children this lane queues in this step
             int32_t lent[4];
 #endif
-            if (state == kTraversing && node >= 0 && np <= kPend - 4) {
+            if (state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
                 const Node4& nd = VR_NODES4[node];
                 if (COUNT) cnt.node_visits++;
@@ -853,9 +863,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // all) are stalled on theirs
             const uint32_t queued = q_tail - q_head;
             if (queued != 0) {
-                const bool stalled = np > 0 && (node < 0 || np > kPend - 4);
+                const bool stalled = np > 0 && (node < 0 || !(VR_ROOM));
                 if (queued >= A.leaf_threshold || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
-                    __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
+                    __ballot(state == kTraversing && node >= 0 && VR_ROOM) == 0) {
                     VR_SEC(0);
                     VR_MARK("leaf_test");
                     leaf_round(queued < 64u ? queued : 64u);
