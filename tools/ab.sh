@@ -12,7 +12,7 @@ for r in $(seq 1 "$R"); do
   for L in "$@"; do
     for sc in $SCENES; do
       VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene ${sc%%:*} --spp ${sc##*:} --reps 2 --variants 0 \
-          --thresholds 56 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
+          --thresholds 52 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
       rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
     done
   done

@@ -760,7 +760,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.error_flag = nullptr;  // per call (enqueue_passes)
     a.fault_object = s->fault_object;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
-    a.shade_threshold = th ? (uint32_t)atoi(th) : 56u;
+    a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
     a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 1u;
     const char* ts = getenv("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end
@@ -779,9 +779,9 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(64, g));
     }
     const char* lt = getenv("VR_LEAF_THRESHOLD");  // tuning hooks
-    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 64u;
+    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = getenv("VR_LEAF_STALL");
-    a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 2u;
+    a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {
