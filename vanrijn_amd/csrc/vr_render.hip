@@ -150,12 +150,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // that reached a leaf in this step.  [slot][thread], LIFO, kPend slots per lane.
 #if VR_WAVE_LEAF
     // per wave: the FIFO of queued leaves (triangle | exact-box flag, and the owning lane) and, per
-    // owner lane, one leaf round's results: entries tested, min distance bits, max rank at that
-    // distance, and that triangle
+    // owner lane, one leaf round's results: entries tested, min distance bits, and (max rank at
+    // that distance, its triangle)
     __shared__ int32_t wl_tri[4 * kWaveList];
     __shared__ uint8_t wl_own[4 * kWaveList];
-    __shared__ unsigned long long lr_d[256];
-    __shared__ uint32_t lr_rank[256], lr_tri[256], lr_cnt[256];
+    __shared__ unsigned long long lr_d[256], lr_key[256];  // key: rank << 32 | triangle
+    __shared__ uint32_t lr_cnt[256];
     const int wbase = (threadIdx.x >> 6) * kWaveList;
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
 #else
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     const unsigned lane = __lane_id();
 #if VR_WAVE_LEAF
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
-    lr_rank[tid] = 0;
+    lr_key[tid] = 0;
     lr_cnt[tid] = 0;
 #endif
     DeviceScene S = A.scene;
@@ -283,9 +283,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         op.o.x = __shfl(pre.o.x, (int)owner);
         op.o.y = __shfl(pre.o.y, (int)owner);
         op.o.z = __shfl(pre.o.z, (int)owner);
-        op.d.x = __shfl(pre.d.x, (int)owner);
-        op.d.y = __shfl(pre.d.y, (int)owner);
-        op.d.z = __shfl(pre.d.z, (int)owner);
+        if (__ballot(mine && e < 0)) {  // the direction only for the exact box test (slab)
+            op.d.x = __shfl(pre.d.x, (int)owner);
+            op.d.y = __shfl(pre.d.y, (int)owner);
+            op.d.z = __shfl(pre.d.z, (int)owner);
+        }
         op.sx = __shfl(pre.sx, (int)owner);
         op.sy = __shfl(pre.sy, (int)owner);
         op.pdz = __shfl(pre.pdz, (int)owner);
@@ -320,9 +322,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         const bool hit = mine && d >= 0.0;
         const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
         if (hit) atomicMin(&lr_d[oslot], bits);
-        const bool at_min = hit && lr_d[oslot] == bits;
-        if (at_min) atomicMax(&lr_rank[oslot], rank);
-        if (at_min && lr_rank[oslot] == rank) lr_tri[oslot] = (uint32_t)tri;
+        // at the minimum distance the highest rank wins; its triangle rides in the low half
+        if (hit && lr_d[oslot] == bits) atomicMax(&lr_key[oslot], ((unsigned long long)rank << 32) | (uint32_t)tri);
         // owners: fold the round's candidate into the closest hit
         const uint32_t got = lr_cnt[tid];
         if (got) {
@@ -330,7 +331,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const unsigned long long db = lr_d[tid];
             if (db != ~0ull) {
                 const double dd = __longlong_as_double((long long)db);
-                const uint32_t rk = lr_rank[tid];
+                const unsigned long long key = lr_key[tid];
+                const uint32_t rk = (uint32_t)(key >> 32);
                 bool take;
                 if (!best.kind || dd < best.d) take = true;
                 else if (dd == best.d)
@@ -339,14 +341,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 if (take) {
                     best.d = dd;
                     best.kind = kTri;
-                    best.index = (int)lr_tri[tid];
+                    best.index = (int)(uint32_t)key;
                     best.object = cur_object;
                     set_cull_far();
                 }
             }
             lr_cnt[tid] = 0;
             lr_d[tid] = ~0ull;
-            lr_rank[tid] = 0;
+            lr_key[tid] = 0;
         }
     };
 #endif
