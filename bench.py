@@ -121,9 +121,12 @@ def valu_issue_cycles(pmc):
     return VALU_CYCLES["other"] * other + VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans
 
 
-def roofline(counts, pixels, kernel_s, key):
+def roofline(counts, pixels, kernel_s, key, passes=1):
+    """kernel_s: the render kernel's time per step (all its launches: a frame whose staging exceeds
+    the per-launch cap runs in `passes` equal launches); the PMC record holds one launch, so its
+    rates use the per-launch time kernel_s / passes."""
     alg = algorithmic_bytes(counts, pixels)
-    r = {"kernel": "render_kernel", "kernel_ms": round(kernel_s * 1e3, 3),
+    r = {"kernel": "render_kernel", "kernel_ms": round(kernel_s * 1e3, 3), "launches_per_step": passes,
          "algorithmic_bytes_per_launch": alg,
          "algorithmic_gbs": round(alg / kernel_s / 1e9, 2),
          "algorithmic_frac": round(alg / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -140,10 +143,11 @@ def roofline(counts, pixels, kernel_s, key):
                   "pmc": f"no PMC record for this library build on '{key}' (tools/pmc.sh)"})
         return r
     pmc = rec["per_launch"]
+    launch_s = kernel_s / max(1, passes)
     traffic = 2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024  # gfx950: FETCH_SIZE counts 128-B lines at 64 B
-    hbm_gbs = traffic / kernel_s / 1e9
+    hbm_gbs = traffic / launch_s / 1e9
     valu = valu_issue_cycles(pmc)
-    valu_rate = valu / kernel_s / 1e9  # G SIMD-cycles of VALU issue per second
+    valu_rate = valu / launch_s / 1e9  # G SIMD-cycles of VALU issue per second
     valu_peak = SIMDS * CLOCK_GHZ
     clk = pmc["GRBM_GUI_ACTIVE"] / 8 / (rec["kernel_ns"] * 1e-9) / 1e9  # effective clock of the profiled launch
     fracs = {"valu": valu_rate / valu_peak, "hbm": hbm_gbs / HBM_PEAK_GBS}
@@ -336,12 +340,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, reduce_ms = [], []
+    kernel_ms, reduce_ms, passes = [], [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(1 + args.warmup + i, timed=True)
         kernel_ms.append(st["kernel_ms"])  # render kernel only (HIP events on the launch stream)
         reduce_ms.append(st["reduce_ms"])  # the ordered per-pixel Kahan reduce after it
+        passes.append(int(st.get("passes", 1)) or 1)  # launches per frame (staging cap)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -382,7 +387,7 @@ def main():
                    "triangles": info["triangle_count"], "bvh_depth": info["max_bvh_depth"],
                    "parallelism": f"spp-split x{world}, RCCL reduce",
                    "pmc_key": config_key(cfg["scene"], W, H, spp)},
-        "roofline": roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp)),
+        "roofline": roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes)),
     }
     out["roofline"]["reduce_kernel_ms"] = round(sum(reduce_ms) / len(reduce_ms), 3)
     if rank == 0 and world == 1 and not args.no_drop_in:
