@@ -625,7 +625,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             __builtin_amdgcn_s_setprio(VR_PRIO_A);
             if (COUNT && first_active_lane()) cnt.outer_slots += 64;
             VR_STAMP(5);
-            if (state == kTraversed) {
+            // shading is deferred while fewer than shade_min lanes have a hit to shade and other
+            // lanes still traverse: the deferred lanes wait (state kTraversed) and the next phase
+            // A shades them with more lanes busy (misses are finished at once either way)
+            bool shade_now = true;
+            if (A.shade_min) {
+                const int nhit = __popcll(__ballot(state == kTraversed && best.kind != kNone));
+                shade_now = nhit >= (int)A.shade_min || __ballot(state == kTraversing) == 0;
+            }
+            if (state == kTraversed && (shade_now || best.kind == kNone)) {
                 VR_MARK("traversed");
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
