@@ -763,6 +763,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
     const char* sm = getenv("VR_SHADE_MIN");  // tuning hook: defer shading below this many hits
     a.shade_min = sm ? (uint32_t)std::max(0, atoi(sm)) : 16u;
+    const char* mm = getenv("VR_MISS_MIN");  // tuning hook: defer finishing misses
+    a.miss_min = mm ? (uint32_t)std::max(0, atoi(mm)) : 8u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
     a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 1u;
     const char* ts = getenv("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end

@@ -144,7 +144,7 @@ struct RenderArgs {
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
-    uint32_t pad_a;
+    uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
     // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
     // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
     double film[4];

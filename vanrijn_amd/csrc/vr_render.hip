@@ -628,12 +628,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // shading is deferred while fewer than shade_min lanes have a hit to shade and other
             // lanes still traverse: the deferred lanes wait (state kTraversed) and the next phase
             // A shades them with more lanes busy (misses are finished at once either way)
-            bool shade_now = true;
-            if (A.shade_min) {
+            bool shade_now = true, finish_now = true;
+            if (A.shade_min | A.miss_min) {
+                const bool idle = __ballot(state == kTraversing) == 0;
                 const int nhit = __popcll(__ballot(state == kTraversed && best.kind != kNone));
-                shade_now = nhit >= (int)A.shade_min || __ballot(state == kTraversing) == 0;
+                const int nmiss = __popcll(__ballot(state == kTraversed && best.kind == kNone));
+                shade_now = nhit >= (int)A.shade_min || idle;
+                finish_now = nmiss >= (int)A.miss_min || idle;
             }
-            if (state == kTraversed && (shade_now || best.kind == kNone)) {
+            if (state == kTraversed && (best.kind == kNone ? finish_now : shade_now)) {
                 VR_MARK("traversed");
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
