@@ -131,3 +131,26 @@ def test_merge_tile_large_tile_threaded(oracle):
         d.weight_buffer[...] = dst.weight_buffer
         d.merge_tile(t, src)
         assert np.array_equal(d.colour_buffer, ref_c) and np.array_equal(d.weight_buffer, ref_w)
+
+
+def test_output_buffers_recycle_only_unreferenced_memory():
+    """partial_render_scene's output buffers reuse memory of dropped buffers, never of live arrays."""
+    import gc
+
+    from vanrijn_amd.render import AccumulationBuffer
+    a = AccumulationBuffer._for_output(40, 20)
+    kept = a.weight_bias_buffer  # the caller keeps one array of an otherwise dropped buffer
+    kept[...] = 7.0
+    del a
+    gc.collect()
+    b = AccumulationBuffer._for_output(40, 20)
+    for arr in (b.colour_buffer, b.colour_sum_buffer, b.colour_bias_buffer, b.weight_buffer, b.weight_bias_buffer):
+        assert not np.shares_memory(arr, kept)
+        arr[...] = -1.0
+    assert (kept == 7.0).all()
+    ptr = b.colour_buffer.ctypes.data
+    del b, arr
+    gc.collect()
+    c = AccumulationBuffer._for_output(40, 20)  # b's store is free again
+    assert c.colour_buffer.ctypes.data == ptr
+    assert c.colour_buffer.shape == (20, 40, 3) and c.weight_buffer.shape == (20, 40)

@@ -9,6 +9,8 @@
 Every render call goes through the C ABI into the gfx950 kernels; nothing here computes a pixel.
 """
 import ctypes as C
+import threading
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -59,6 +61,48 @@ class TileIterator:
             row += self.s
 
 
+class _OutputPool:
+    """Backing stores for output AccumulationBuffers (11 f64 per pixel).  A store is handed out
+    again only when every view made from it has been garbage-collected (weak references), so a
+    caller holding any array of an old buffer keeps its memory to itself."""
+
+    def __init__(self, keep=32):
+        self.keep = keep
+        self.lock = threading.Lock()
+        self.stores = []  # [backing array, [weakref per view]]
+
+    @staticmethod
+    def _split(store, width, height):
+        n = width * height
+        return (store[0:3 * n].reshape(height, width, 3), store[3 * n:6 * n].reshape(height, width, 3),
+                store[6 * n:9 * n].reshape(height, width, 3), store[9 * n:10 * n].reshape(height, width),
+                store[10 * n:11 * n].reshape(height, width))
+
+    def views(self, width, height):
+        size = 11 * width * height
+        with self.lock:
+            for entry in self.stores:
+                if entry[0].size == size and all(r() is None for r in entry[1]):
+                    vs = self._split(entry[0], width, height)
+                    entry[1] = [weakref.ref(v) for v in vs]
+                    return vs
+        store = np.empty(size)
+        vs = self._split(store, width, height)
+        with self.lock:
+            self.stores.append([store, [weakref.ref(v) for v in vs]])
+            if len(self.stores) > self.keep:  # drop a free store (or the oldest record of one)
+                for i, e in enumerate(self.stores):
+                    if all(r() is None for r in e[1]):
+                        del self.stores[i]
+                        break
+                else:
+                    del self.stores[0]
+        return vs
+
+
+_OUTPUT_POOL = _OutputPool()
+
+
 class AccumulationBuffer:
     """Per-pixel Kahan-compensated XYZ sums and weights; `colour` is the running mean.
 
@@ -80,14 +124,12 @@ class AccumulationBuffer:
 
     @classmethod
     def _for_output(cls, width, height):
-        """A buffer the library overwrites completely (all five arrays): allocated without the
-        zeroing pass, which cost as much host time as the render itself at 1 spp."""
+        """A buffer the library overwrites completely (all five arrays): no zeroing pass, and its
+        memory recycled from buffers nobody references any more (_OutputPool) -- fresh pages cost
+        a page fault per 4 KB on first write, as much host time as a 1-spp render itself."""
         b = cls.__new__(cls)
-        b.colour_buffer = np.empty((height, width, 3))
-        b.colour_sum_buffer = np.empty((height, width, 3))
-        b.colour_bias_buffer = np.empty((height, width, 3))
-        b.weight_buffer = np.empty((height, width))
-        b.weight_bias_buffer = np.empty((height, width))
+        (b.colour_buffer, b.colour_sum_buffer, b.colour_bias_buffer, b.weight_buffer,
+         b.weight_bias_buffer) = _OUTPUT_POOL.views(width, height)
         return b
 
     def width(self):
