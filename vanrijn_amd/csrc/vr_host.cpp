@@ -1339,7 +1339,13 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
     if (npix == 0 || p->spp == 0) return VR_OK;
     size_t free_b = 0, total_b = 0;
     VR_HIP(hipMemGetInfo(&free_b, &total_b));
-    const size_t cap = std::min<size_t>((size_t)16 << 30, (free_b + c->staging_bytes) / 2);
+    // staging for a whole frame when half the free HBM holds it (a 288 GB MI355X: C4 / C5's
+    // 68.7 GB on one GPU in one launch -- every extra launch adds the tail of the frame's longest
+    // paths, ~7 ms on the C5 mesh); VR_STAGING_CAP_MB lowers the cap (tests of the pass split)
+    const char* cap_mb = getenv("VR_STAGING_CAP_MB");
+    const size_t cap_env = cap_mb ? (size_t)std::max(1LL, atoll(cap_mb)) << 20 : 0;
+    size_t cap = (free_b + c->staging_bytes) / 2;
+    if (cap_env) cap = std::min(cap, cap_env);
     uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (16 * npix)));
     // the kernel decodes work items with 32-bit block indices: (8x8 blocks) x samples < 2^32
     if (((tw + 7) / 8) * ((th + 7) / 8) * pass >= (1ull << 32))
