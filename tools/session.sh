@@ -36,6 +36,9 @@ for s in $STEPS; do
     cycles)
       timeout -k 10 300 python tools/cycles.py 64 main > gpurun_out/${TAG}_cycles_main.json 2> gpurun_out/${TAG}_cycles.err
       rc=$?; echo "cycles rc=$rc" ;;
+    tail)
+      timeout -k 10 300 python tools/wg_tail.py 256 main > gpurun_out/${TAG}_tail_main.json 2> gpurun_out/${TAG}_tail.err
+      rc=$?; echo "tail rc=$rc"; cat gpurun_out/${TAG}_tail_main.json ;;
     dropin)
       timeout -k 10 400 python tools/dropin.py 1024 32 > gpurun_out/${TAG}_dropin.json 2> gpurun_out/${TAG}_dropin.err
       rc=$?; echo "dropin rc=$rc"; tail -1 gpurun_out/${TAG}_dropin.json ;;
