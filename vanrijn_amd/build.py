@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvanrijn_amd.so")
 SOURCES = ["vr_render.hip", "vr_image.hip", "vr_build.hip", "vr_host.cpp"]
-HEADERS = ["vr_layout.h", "vr_device.h", "rgb_spectrum_tables.h", os.path.join("..", "..", "include", "vanrijn_amd.h")]
+HEADERS = ["vr_layout.h", "vr_device.h", "rgb_spectrum_tables.h", "vr_exp_table.h", os.path.join("..", "..", "include", "vanrijn_amd.h")]
 
 FLAGS = [
     "--offload-arch=gfx950",

@@ -230,20 +230,23 @@ __device__ __forceinline__ double gaussian(double wl, double alpha, double mu, d
     return alpha * exp(-(t * t) / denominator);
 }
 // The ordered reduce's form: exp(-(t^2) * k) with k = 1 / (2 s^2) a compile-time constant per lobe
-// side instead of a division per lobe (7 per sample, a quarter of the reduce's instructions); the
-// colour is an output value only, within 1e-14 relative of xyz_for_wavelength
-__device__ __forceinline__ double gaussian_k(double wl, double alpha, double mu, double k1, double k2) {
+// side instead of a division per lobe, and the table-driven exp (vr_exp_table.h, within 2 ulp of
+// exp): the colour is an output value only, within 1e-14 relative of xyz_for_wavelength.
+// `tab` holds VR_EXP_TABLE_INIT (the reduce keeps it in LDS)
+__device__ __forceinline__ double gaussian_kt(double wl, double alpha, double mu, double k1, double k2,
+                                              const double* tab) {
     const double k = wl < mu ? k1 : k2;
     const double t = wl - mu;
-    return alpha * exp(-(t * t) * k);
+    return alpha * vr_exp_tab(-(t * t) * k, tab);
 }
-#define VR_G(alpha, mu, s1, s2) gaussian_k(wl, alpha, mu, 1.0 / (2.0 * ((s1) * (s1))), 1.0 / (2.0 * ((s2) * (s2))))
-__device__ __forceinline__ V3 xyz_for_wavelength_fast(double wl) {
-    return mk(VR_G(1.056, 599.8, 37.9, 31.0) + VR_G(0.362, 442.0, 16.0, 26.7) + VR_G(-0.065, 501.1, 20.4, 26.2),
-              VR_G(0.821, 568.8, 46.9, 40.5) + VR_G(0.286, 530.9, 16.3, 31.1),
-              VR_G(1.217, 437.0, 11.8, 36.0) + VR_G(0.681, 459.0, 26.0, 13.8));
+#define VR_GT(alpha, mu, s1, s2) \
+    gaussian_kt(wl, alpha, mu, 1.0 / (2.0 * ((s1) * (s1))), 1.0 / (2.0 * ((s2) * (s2))), tab)
+__device__ __forceinline__ V3 xyz_for_wavelength_tab(double wl, const double* tab) {
+    return mk(VR_GT(1.056, 599.8, 37.9, 31.0) + VR_GT(0.362, 442.0, 16.0, 26.7) + VR_GT(-0.065, 501.1, 20.4, 26.2),
+              VR_GT(0.821, 568.8, 46.9, 40.5) + VR_GT(0.286, 530.9, 16.3, 31.1),
+              VR_GT(1.217, 437.0, 11.8, 36.0) + VR_GT(0.681, 459.0, 26.0, 13.8));
 }
-#undef VR_G
+#undef VR_GT
 __device__ __forceinline__ V3 xyz_for_wavelength(double wl) {
     return mk(gaussian(wl, 1.056, 599.8, 37.9, 31.0) + gaussian(wl, 0.362, 442.0, 16.0, 26.7) +
                   gaussian(wl, -0.065, 501.1, 20.4, 26.2),

@@ -31,6 +31,7 @@
 #include "../../include/vanrijn_amd.h"
 #include "rgb_spectrum_tables.h"
 #include "vr_layout.h"
+#include "vr_exp_table.h"
 
 #include "vr_device.h"
 
@@ -942,8 +943,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 typedef double d2 __attribute__((ext_vector_type(2)));
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
+__constant__ double c_exp_tab[64] = VR_EXP_TABLE_INIT;
 __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const double* staging, uint64_t npix,
                                                          uint32_t spp, uint32_t accumulate) {
+    __shared__ double etab[64];  // 2^(j/64) for the lobes' exp (vr_exp_table.h)
+    if (threadIdx.x < 64) etab[threadIdx.x] = c_exp_tab[threadIdx.x];
+    __syncthreads();
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
     double sum[3] = {0.0, 0.0, 0.0}, bias[3] = {0.0, 0.0, 0.0}, w = 0.0, wb = 0.0;
@@ -982,7 +987,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
             const d2 v = __builtin_nontemporal_load(ph);
             const double wl = v.x, I = v.y;
             const double Is = I * 360.0;                // photon.rs:26-28, camera.rs:121-126
-            const V3 cx = xyz_for_wavelength_fast(wl);  // colour_xyz.rs:31-35
+            const V3 cx = xyz_for_wavelength_tab(wl, etab);  // colour_xyz.rs:31-35
             c[j][0] = cx.x * Is;
             c[j][1] = cx.y * Is;
             c[j][2] = cx.z * Is;
@@ -994,7 +999,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
         const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)s * npix + p));
         const double wl = v.x, I = v.y;
         const double Is = I * 360.0;
-        const V3 cx = xyz_for_wavelength_fast(wl);
+        const V3 cx = xyz_for_wavelength_tab(wl, etab);
         const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
         update(c);
     }
