@@ -980,17 +980,30 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     uint32_t s = 0;
     for (; s + kB <= spp; s += kB) {
         double c[kB][3];
+        d2 v[kB];
+        bool dark = true;
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             // final photon {wavelength, intensity}: one 16-B non-temporal load
-            const d2* ph = reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p);
-            const d2 v = __builtin_nontemporal_load(ph);
-            const double wl = v.x, I = v.y;
-            const double Is = I * 360.0;                // photon.rs:26-28, camera.rs:121-126
-            const V3 cx = xyz_for_wavelength_tab(wl, etab);  // colour_xyz.rs:31-35
-            c[j][0] = cx.x * Is;
-            c[j][1] = cx.y * Is;
-            c[j][2] = cx.z * Is;
+            v[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p));
+            dark = dark && __double_as_longlong(v[j].x) == 0 && __double_as_longlong(v[j].y) == 0;
+        }
+        if (__ballot(!dark) == 0) {
+            // a missed camera ray's photon {+0, +0} (camera.rs:110-113): every lobe is positive at
+            // 0 nm, so its colour is (+0, +0, +0) exactly -- the wave skips the 28 exp when all
+            // its photons are such (rows of pixels that see no geometry)
+#pragma unroll
+            for (uint32_t j = 0; j < kB; ++j) c[j][0] = c[j][1] = c[j][2] = 0.0;
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kB; ++j) {
+                const double wl = v[j].x, I = v[j].y;
+                const double Is = I * 360.0;                     // photon.rs:26-28, camera.rs:121-126
+                const V3 cx = xyz_for_wavelength_tab(wl, etab);  // colour_xyz.rs:31-35
+                c[j][0] = cx.x * Is;
+                c[j][1] = cx.y * Is;
+                c[j][2] = cx.z * Is;
+            }
         }
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) update(c[j]);
