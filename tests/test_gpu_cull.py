@@ -1,0 +1,47 @@
+"""Camera-frustum culling of 8x8 pixel blocks changes no bit of the accumulation records.
+
+block_cull_kernel (vr_render.hip) marks the blocks of a launch's tile whose camera rays all miss
+every object by a wide margin; the render kernel skips their work items and the ordered reduce
+applies their samples as the missed camera ray's photon {0, 0} (camera.rs:110-113) without staged
+data.  The records must equal a render with the test off (VR_BLOCK_CULL=0), on a full frame, on a
+tile whose edges cut 8x8 blocks, and for an accumulating continuation (non-zero Kahan
+compensations, accumulation_buffer.rs:44-60).
+"""
+import pytest
+import torch
+
+from vanrijn_amd import scenes
+from vanrijn_amd.render import Tile, render_tile_device
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def device_scenes():
+    return {"main": scenes.main_scene().device_scene(0), "bench": scenes.bench_scene().device_scene(0)}
+
+
+@pytest.mark.parametrize("which,tile,hw", [("main", (0, 512, 0, 512), (512, 512)),
+                                           ("bench", (37, 333, 11, 250), (300, 400)),
+                                           ("main", (5, 203, 100, 300), (300, 400))])
+def test_cull_is_bit_identical(which, tile, hw, device_scenes, monkeypatch):
+    ds = device_scenes[which]
+    t = Tile(*tile)
+    H, W = hw
+    npix = (t.end_column - t.start_column) * (t.end_row - t.start_row)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def run(cull):
+        monkeypatch.setenv("VR_BLOCK_CULL", "1" if cull else "0")
+        st = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
+        render_tile_device(ds, t, H, W, 4, 0x77, 0, st.data_ptr(), stream)
+        render_tile_device(ds, t, H, W, 3, 0x77, 4, st.data_ptr(), stream, accumulate=True)
+        c = render_tile_device(ds, t, H, W, 2, 0x77, 7, st.data_ptr(), stream, accumulate=True, counters=True)
+        torch.cuda.synchronize()
+        return st.cpu(), c
+
+    (a, ca), (b, cb) = run(False), run(True)
+    assert torch.equal(a, b)
+    assert ca["samples"] == npix * 2
+    if which == "bench" or tile[2] == 0:  # the sky above the scene is culled there
+        assert cb["samples"] < ca["samples"]

@@ -485,6 +485,8 @@ struct CallCtx {
     size_t scratch_bytes = 0;
     void* pinned = nullptr;  // page-locked host copy of the host-layout buffers (DMA at full PCIe rate)
     size_t pinned_bytes = 0;
+    void* mask = nullptr;  // camera-frustum culled 8x8 blocks of the call's tile (1 B each)
+    size_t mask_bytes = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -758,6 +760,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.counters = nullptr;
     a.wg_times = nullptr;
     a.error_flag = nullptr;  // per call (enqueue_passes)
+    a.block_mask = nullptr;  // per call (enqueue_passes)
     a.fault_object = s->fault_object;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
@@ -855,6 +858,7 @@ void ctx_free_all(CallCtx* c) {
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->staging) (void)hipFree(c->staging);
+    if (c->mask) (void)hipFree(c->mask);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->queue) (void)hipFree(c->queue);
@@ -1354,6 +1358,18 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
     int rc = ctx_grow(&c->staging, &c->staging_bytes, (size_t)(16 * npix * pass), c->done);
     if (rc) return rc;
+    // blocks whose camera rays all miss every object (one small kernel per call; VR_BLOCK_CULL=0
+    // turns the test off)
+    const bool cull = !(getenv("VR_BLOCK_CULL") && atoi(getenv("VR_BLOCK_CULL")) == 0);
+    const uint8_t* mask = nullptr;
+    if (cull && !recording) {  // (the record variant writes every sample's record)
+        rc = ctx_grow(&c->mask, &c->mask_bytes, (size_t)(((tw + 7) / 8) * ((th + 7) / 8)), c->done);
+        if (rc) return rc;
+        vr::RenderArgs a = make_args(s, p, state);
+        const int lc = vr::launch_block_cull(a, (uint8_t*)c->mask, st);
+        if (lc) return fail(VR_ERROR_DEVICE, vr::device_error_string(lc));
+        mask = (const uint8_t*)c->mask;
+    }
     for (uint64_t done = 0; done < p->spp; done += pass) {
         vr_render_params q = *p;
         q.spp = (uint32_t)std::min<uint64_t>(pass, p->spp - done);
@@ -1363,6 +1379,7 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         a.staging = (double*)c->staging;
         a.queue = c->queue;
         a.error_flag = err;
+        a.block_mask = mask;
         a.records = records;
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;

@@ -158,6 +158,9 @@ struct RenderArgs {
     unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
     unsigned long long* wg_times;  // counting variant: [blocks][2] s_memrealtime at start / end, or nullptr
     int32_t* error_flag;          // this call's error word (a singular shading basis sets it)
+    // per 8x8 pixel block of the tile: 1 when every camera ray through the block provably misses
+    // every object (block_cull_kernel), so each of its samples is photon {0, 0}; nullptr: none
+    const uint8_t* block_mask;
 };
 
 struct TraceArgs {
@@ -191,6 +194,8 @@ enum Counter : int {
 int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
                   int grid_limit, void* stream, void* mid_event = nullptr);
 // vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
+// the camera-frustum test of every 8x8 block of a launch's tile into mask (RenderArgs::block_mask)
+int launch_block_cull(const RenderArgs& args, uint8_t* mask, void* stream);
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
 // vr_image.hip: device records (8 f64 per pixel) <-> the host AccumulationBuffer's five arrays laid
 // out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read;

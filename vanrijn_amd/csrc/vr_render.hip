@@ -722,7 +722,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         if (bx < 0) { --by; bx += (int32_t)bw; }
                         if (bx >= (int32_t)bw) { ++by; bx -= (int32_t)bw; }
                         const uint32_t x = (uint32_t)bx * 8 + (l & 7), y = by * 8 + (l >> 3);
-                        if (x < A.tile_width && y < A.tile_height) {  // else: padding, take another item
+                        // else padding, or a block whose camera rays all miss every object (its
+                        // samples are the photon {0, 0}: the ordered reduce applies them without
+                        // staged data): take another item
+                        if (x < A.tile_width && y < A.tile_height && !(kargs()->block_mask && kargs()->block_mask[blk])) {
                             px = x;
                             py = y;
                             if (chunk_i < rounds) {
@@ -940,12 +943,93 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #undef VR_STAMP
 #undef VR_SEC
 
+// Camera-frustum test of the tile's 8x8 pixel blocks (one thread per block).  The camera rays of a
+// block start at the camera and pass through the film rectangle its pixels' sample squares cover
+// (camera.rs:24-66: x = (col + u) fw/w - fw/2, y = (h - row - 1 + v) fh/h - fh/2, u, v in [0, 1),
+// direction (x, y, 1) normalised).  A block is culled only when every such line provably misses
+// every object, with margins far beyond the f64 rounding of the reference's tests:
+//  * a plane (plane.rs:49-75): its t = num / dn is negative for every ray -- num and n . (x, y, 1)
+//    of opposite signs at all four corners of the rectangle (a linear function: its extremes),
+//    each by more than 1e-9 of its magnitude scale;
+//  * a sphere, or a BVH root box through its bounding sphere (a ray that misses the box misses
+//    every triangle in it): the camera is outside it and the angle between the sphere's centre and
+//    the axis of the block's cone of directions exceeds the cone's half-angle (attained at a
+//    corner) plus the sphere's angular radius plus 1e-6 rad.
+// Each sample of a culled block is then exactly the missed camera ray's photon {0, 0}, whatever
+// its random draws.
+__device__ __forceinline__ double vr_angle(V3 a, V3 b) {
+    return atan2(sqrt(dot(cross(a, b), cross(a, b))), dot(a, b));
+}
+__global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Prim* prims, const Bvh* bvhs,
+                                                         uint8_t* mask) {
+    const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= bw * bh) return;
+    const uint32_t bx = b % bw, by = b / bw;
+    const double c0 = (double)(A.start_column + 8 * (uint64_t)bx);
+    const double c1 = (double)(A.start_column + min((uint64_t)8 * bx + 8, A.tile_width));
+    const double r0 = (double)(A.start_row + 8 * (uint64_t)by);
+    const double r1 = (double)(A.start_row + min((uint64_t)8 * by + 8, A.tile_height));
+    const double H = (double)A.height;
+    const double xa = c0 * A.film[0] - A.film[1], xb = c1 * A.film[0] - A.film[1];
+    const double ya = (H - r1) * A.film[2] - A.film[3], yb = (H - r0) * A.film[2] - A.film[3];
+    const double mx = 1e-9 * (fabs(xa) + fabs(xb) + 1.0), my = 1e-9 * (fabs(ya) + fabs(yb) + 1.0);
+    const double xlo = fmin(xa, xb) - mx, xhi = fmax(xa, xb) + mx;
+    const double ylo = fmin(ya, yb) - my, yhi = fmax(ya, yb) + my;
+    const V3 pc[4] = {mk(xlo, ylo, 1.0), mk(xhi, ylo, 1.0), mk(xlo, yhi, 1.0), mk(xhi, yhi, 1.0)};
+    V3 axis = mk(0.0, 0.0, 0.0);
+    for (int i = 0; i < 4; ++i) axis = add(axis, normalize(pc[i]));
+    axis = normalize(axis);
+    double half = 0.0;
+    for (int i = 0; i < 4; ++i) half = fmax(half, vr_angle(axis, pc[i]));
+    const V3 o = mk(A.scene.camera[0], A.scene.camera[1], A.scene.camera[2]);
+    // a sphere (centre c, radius r) every ray of the block misses
+    auto sphere_clear = [&](V3 c, double r) {
+        const V3 v = sub(c, o);
+        const double dist = sqrt(dot(v, v));
+        if (!(dist > r * (1.0 + 1e-6) + 1e-9)) return false;
+        return vr_angle(axis, v) > half + asin(fmin(1.0, r / dist)) + 1e-6;
+    };
+    bool clear = true;
+    for (int i = 0; i < A.scene.prim_count && clear; ++i) {
+        const Prim& pr = prims[i];
+        const V3 c = ldv(pr.vec);
+        if (pr.kind == 0) {
+            const V3 q = ldv(pr.pre);
+            const double num = dot(sub(q, o), c);
+            const double nn = sqrt(dot(c, c));
+            const double tol = 1e-9 * nn * (sqrt(dot(q, q)) + sqrt(dot(o, o)) + 1.0);
+            if (!(fabs(num) > tol)) {
+                clear = false;
+                break;
+            }
+            for (int k = 0; k < 4; ++k) {
+                const double dn = dot(pc[k], c);
+                const double t = 1e-9 * nn * sqrt(dot(pc[k], pc[k]));
+                if (!(num > 0.0 ? dn < -t : dn > t)) clear = false;
+            }
+        } else {
+            clear = sphere_clear(c, pr.scalar);
+        }
+    }
+    for (int i = 0; i < A.scene.bvh_count && clear; ++i) {
+        const Bvh& bv = bvhs[i];
+        if (bv.root4 == INT32_MIN) continue;  // an empty mesh never hits
+        const double* bb = bv.root_box;
+        const V3 c = mk(0.5 * (bb[0] + bb[1]), 0.5 * (bb[2] + bb[3]), 0.5 * (bb[4] + bb[5]));
+        const V3 e = mk(bb[1] - bb[0], bb[3] - bb[2], bb[5] - bb[4]);
+        clear = sphere_clear(c, 0.5 * sqrt(dot(e, e)) * (1.0 + 1e-9) + 1e-12);
+    }
+    mask[b] = clear ? 1 : 0;
+}
+
 typedef double d2 __attribute__((ext_vector_type(2)));
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
 __constant__ double c_exp_tab[64] = VR_EXP_TABLE_INIT;
 __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const double* staging, uint64_t npix,
-                                                         uint32_t spp, uint32_t accumulate) {
+                                                         uint32_t spp, uint32_t accumulate, const uint8_t* mask,
+                                                         uint64_t tile_width) {
     __shared__ double etab[64];  // 2^(j/64) for the lobes' exp (vr_exp_table.h)
     if (threadIdx.x < 64) etab[threadIdx.x] = c_exp_tab[threadIdx.x];
     __syncthreads();
@@ -978,6 +1062,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     // order -- the same operations as one at a time, with kB-fold instruction-level parallelism
     constexpr uint32_t kB = 4;
     uint32_t s = 0;
+    if (mask) {
+        const uint64_t py = p / tile_width, px = p - py * tile_width;
+        if (mask[(py >> 3) * ((tile_width + 7) >> 3) + (px >> 3)]) {
+            // a culled block (block_cull_kernel): every sample is the photon {0, 0}, colour +0
+            const double z[3] = {0.0, 0.0, 0.0};
+            for (; s < spp; ++s) update(z);
+        }
+    }
     for (; s + kB <= spp; s += kB) {
         double c[kB][3];
         d2 v[kB];
@@ -1090,7 +1182,7 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
         }
         const uint64_t npix = a.tile_width * a.tile_height;
         hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
-                           (const double*)a.staging, npix, a.spp, a.accumulate);
+                           (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width);
         return hipGetLastError();
     }
 #define VR_LAUNCH(C, R, D, M, W)                                                                      \
@@ -1129,8 +1221,16 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     }
     const uint64_t npix = a.tile_width * a.tile_height;
     hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
-                       (const double*)a.staging, npix, a.spp, a.accumulate);
+                       (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width);
     return hipGetLastError();
+}
+
+int launch_block_cull(const RenderArgs& a, uint8_t* mask, void* stream) {
+    const uint64_t blocks = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8);
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(dev::block_cull_kernel, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       a, a.scene.prims, a.scene.bvhs, mask);
+    return (int)hipGetLastError();
 }
 
 int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int mats,
