@@ -390,6 +390,10 @@ def main():
         "roofline": roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes)),
     }
     out["roofline"]["reduce_kernel_ms"] = round(sum(reduce_ms) / len(reduce_ms), 3)
+    # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied
+    # as the photon {0, 0} without tracing: the records are bit-identical with VR_BLOCK_CULL=0
+    # (tests/test_gpu_cull.py); every sample is counted in `value`
+    out["roofline"]["frustum_culled_sample_fraction"] = round(1.0 - counts["samples"] / (W * H * spp), 4)
     if rank == 0 and world == 1 and not args.no_drop_in:
         out["drop_in"] = drop_in_leg(dscene, W, H, args.drop_in_frames, args.drop_in_threads, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
