@@ -951,10 +951,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 //  * a plane (plane.rs:49-75): its t = num / dn is negative for every ray -- num and n . (x, y, 1)
 //    of opposite signs at all four corners of the rectangle (a linear function: its extremes),
 //    each by more than 1e-9 of its magnitude scale;
-//  * a sphere, or a BVH root box through its bounding sphere (a ray that misses the box misses
-//    every triangle in it): the camera is outside it and the angle between the sphere's centre and
-//    the axis of the block's cone of directions exceeds the cone's half-angle (attained at a
-//    corner) plus the sphere's angular radius plus 1e-6 rad.
+//  * a BVH root box (a ray that misses the box misses every triangle in it) wholly in front of the
+//    camera: the bounding rectangle of its corners' film projections (x/z, y/z), widened by 1e-6,
+//    misses the block's film rectangle;
+//  * a sphere, or a root box through its bounding sphere: the camera is outside it and the angle
+//    between the sphere's centre and the axis of the block's cone of directions exceeds the cone's
+//    half-angle (attained at a corner) plus the sphere's angular radius plus 1e-6 rad.
 // Each sample of a culled block is then exactly the missed camera ray's photon {0, 0}, whatever
 // its random draws.
 __device__ __forceinline__ double vr_angle(V3 a, V3 b) {
@@ -1016,6 +1018,23 @@ __global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Pri
         const Bvh& bv = bvhs[i];
         if (bv.root4 == INT32_MIN) continue;  // an empty mesh never hits
         const double* bb = bv.root_box;
+        // a box wholly in front of the camera: the directions that reach it project (x/z, y/z)
+        // into the bounding rectangle of its corners' projections; clear when that rectangle,
+        // widened by 1e-6 of its scale, misses the block's film rectangle
+        double ulo = INFINITY, uhi = -INFINITY, vlo = INFINITY, vhi = -INFINITY;
+        bool front = true;
+        for (int k = 0; k < 8; ++k) {
+            const double px = bb[k & 1] - o.x, py = bb[2 + ((k >> 1) & 1)] - o.y, pz = bb[4 + (k >> 2)] - o.z;
+            front = front && pz > 1e-6 * (fabs(px) + fabs(py) + fabs(pz));
+            ulo = fmin(ulo, px / pz);
+            uhi = fmax(uhi, px / pz);
+            vlo = fmin(vlo, py / pz);
+            vhi = fmax(vhi, py / pz);
+        }
+        if (front) {
+            const double mu = 1e-6 * (fabs(ulo) + fabs(uhi) + 1.0), mv = 1e-6 * (fabs(vlo) + fabs(vhi) + 1.0);
+            if (uhi + mu < xlo || ulo - mu > xhi || vhi + mv < ylo || vlo - mv > yhi) continue;
+        }
         const V3 c = mk(0.5 * (bb[0] + bb[1]), 0.5 * (bb[2] + bb[3]), 0.5 * (bb[4] + bb[5]));
         const V3 e = mk(bb[1] - bb[0], bb[3] - bb[2], bb[5] - bb[4]);
         clear = sphere_clear(c, 0.5 * sqrt(dot(e, e)) * (1.0 + 1e-9) + 1e-12);
