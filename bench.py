@@ -310,7 +310,10 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
-    if world > 1:
+    # launched by torch.distributed.run (RANK set): the RCCL group is created even at world size 1,
+    # so a one-GPU box rehearses the multi-GPU step (init, barriers, reduce, max-over-ranks timing)
+    distributed = world > 1 or "RANK" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H = cfg["width"], cfg["height"]
@@ -337,7 +340,7 @@ def main():
     for i in range(args.warmup):
         step(1 + i)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     kernel_ms, reduce_ms, passes = [], [], []
@@ -348,12 +351,12 @@ def main():
         reduce_ms.append(st["reduce_ms"])  # the ordered per-pixel Kahan reduce after it
         passes.append(int(st.get("passes", 1)) or 1)  # launches per frame (staging cap)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     stream_check_error(dscene, stream.cuda_stream, device=local)  # device errors of the untimed steps
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -403,7 +406,7 @@ def main():
         out["cpu_baseline"]["host"] = ci
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -42,6 +42,13 @@ for s in $STEPS; do
     dropin)
       timeout -k 10 400 python tools/dropin.py 1024 32 > gpurun_out/${TAG}_dropin.json 2> gpurun_out/${TAG}_dropin.err
       rc=$?; echo "dropin rc=$rc"; tail -1 gpurun_out/${TAG}_dropin.json ;;
+    dist)
+      # bench.py under torch.distributed.run at world size 1: the RCCL group, barriers, the
+      # records' dist.reduce and the max-over-ranks timing that the 8-GPU runs take
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+          --master-port 29517 bench.py --config $cfg --gpus 1 --steps 2 --warmup 1 --no-cpu-baseline --no-drop-in \
+          > gpurun_out/${TAG}_dist_$cfg.json 2> gpurun_out/${TAG}_dist_$cfg.err
+      rc=$?; echo "dist $cfg rc=$rc"; cut -c 1-300 gpurun_out/${TAG}_dist_$cfg.json; tail -3 gpurun_out/${TAG}_dist_$cfg.err ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1; rc=$?; echo "list rc=$rc" ;;
     *) echo "unknown step $s"; rc=2 ;;

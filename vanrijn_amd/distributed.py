@@ -47,7 +47,9 @@ def reduce_records(state: torch.Tensor, dst=0, group=None):
     (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
     reduced state then starts a fresh compensated sum from the merged totals."""
     rank, world = world_info(group)
-    if world > 1:
+    # through the collective whenever a group exists (at world size 1 too: bench.py under
+    # torch.distributed.run on one GPU rehearses the RCCL step the 8-GPU runs take)
+    if dist.is_available() and dist.is_initialized():
         dist.reduce(state, dst=dst, op=dist.ReduceOp.SUM, group=group)
         if rank == dst:
             s = state.view(-1, RECORD)
