@@ -486,6 +486,30 @@ __device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p) 
                      (float)s.vec[2] * (float)s.vec[2];
     return (oc2 - t * t) - r * r > 1e-4f * oc2 + 1e-12f * (po + pc);
 }
+// sphere_missed32, or the sphere cannot become the closest hit: it lies wholly behind the origin
+// (both roots negative: distance <= 0, None), or its near root lies beyond `best` (the distance
+// the sphere must beat: dd < best fails, the first of equals is kept).  The exact roots are
+// -t -+ sqrt(r^2 - dist^2) (|d| = 1), so both are < 0 when t > r and the near one exceeds
+// -t - r.  The reference's f64 roots err by at most ~5e-8 sqrt(|o|^2 + |c|^2 + |oc|^2) (its
+// discriminant's rounding under the sqrt) and this f32 t by < 3e-7 |oc|_1: the margin
+// m = 1e-4 |oc|_1 + 1e-6 (|o|_1 + |c|_1 + r) covers both (L1 norms bound L2).  best = +inf: no
+// best yet.  NaN anywhere: not skipped.
+__device__ __forceinline__ bool sphere_skip32(const Prim& s, const RayPre& p, float best) {
+    const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
+    const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
+    const float t = ox * dx + oy * dy + oz * dz;
+    const float oc2 = ox * ox + oy * oy + oz * oz;
+    const float r = (float)s.scalar;
+    const float po = (float)p.o.x * (float)p.o.x + (float)p.o.y * (float)p.o.y + (float)p.o.z * (float)p.o.z;
+    const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
+                     (float)s.vec[2] * (float)s.vec[2];
+    if ((oc2 - t * t) - r * r > 1e-4f * oc2 + 1e-12f * (po + pc)) return true;
+    const float m = 1e-4f * (fabsf(ox) + fabsf(oy) + fabsf(oz)) +
+                    1e-6f * (fabsf((float)p.o.x) + fabsf((float)p.o.y) + fabsf((float)p.o.z) +
+                             fabsf((float)s.vec[0]) + fabsf((float)s.vec[1]) + fabsf((float)s.vec[2]) + r);
+    if (t - r > m) return true;                                   // behind the origin
+    return (-t - r) - m > best + 1e-6f * fabsf(best) + 1e-30f;  // beyond the best distance
+}
 
 // Plane::intersect (plane.rs:49-75): t or -1 (t == 0 is a hit).  NaN t (ray inside the plane)
 // is reported as a hit with NaN distance, as in the reference; it never wins a comparison here.

@@ -104,6 +104,12 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_PRIO_LEAF
 #define VR_PRIO_LEAF 1
 #endif
+#ifndef VR_SPHERE_SKIP  // f32 sphere skip: line miss, behind the origin or beyond the best hit
+#define VR_SPHERE_SKIP 0
+#endif
+#ifndef VR_LATE_BOX  // leaf round: the exact box test only for entries whose triangle hits
+#define VR_LATE_BOX 1
+#endif
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
@@ -284,11 +290,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         op.o.x = __shfl(pre.o.x, (int)owner);
         op.o.y = __shfl(pre.o.y, (int)owner);
         op.o.z = __shfl(pre.o.z, (int)owner);
+#if !VR_LATE_BOX
         if (__ballot(mine && e < 0)) {  // the direction only for the exact box test (slab)
             op.d.x = __shfl(pre.d.x, (int)owner);
             op.d.y = __shfl(pre.d.y, (int)owner);
             op.d.z = __shfl(pre.d.z, (int)owner);
         }
+#endif
         op.sx = __shfl(pre.sx, (int)owner);
         op.sy = __shfl(pre.sy, (int)owner);
         op.pdz = __shfl(pre.pdz, (int)owner);
@@ -297,6 +305,42 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         double d = -1.0;
         uint32_t rank = 0;
         const int tri = e & 0x7fffffff;
+#if VR_LATE_BOX
+        // The exact box test decides only where the triangle test hits: a leaf whose triangle
+        // misses adds nothing whichever way its box test goes (bvh.rs:77-120 tests the triangle only
+        // inside a hit box), so the reference's box decision is taken after the triangle test and
+        // only for hitting entries -- the wave runs the six f64 divisions only when such an entry
+        // exists, not whenever an entry's f32 box test was too close to call.  The counting variant
+        // tests every flagged box, so its counters stay the reference's.
+        TriVerts tv;
+        if (mine) {
+            tv = load_tri(VR_TRIS + tri);
+            double b[3];
+            d = triangle_distance(tv, op, b);  // needs the owner's shear constants, not its direction
+            rank = (uint32_t)tv.rank;
+            if (COUNT && e >= 0) cnt.tri_tests++;
+        }
+        if (__ballot(mine && e < 0 && (COUNT || d >= 0.0))) {
+            op.d.x = __shfl(pre.d.x, (int)owner);
+            op.d.y = __shfl(pre.d.y, (int)owner);
+            op.d.z = __shfl(pre.d.z, (int)owner);
+            if (mine && e < 0 && (COUNT || d >= 0.0)) {  // the leaf's f32 box test was too close to call
+                VR_SEC(2);
+                VR_MARK("exact_box");
+                if (COUNT) cnt.exact_boxes++;
+                double bb[6], lo, hi;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    bb[2 * a] = fmin(fmin(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                    bb[2 * a + 1] = fmax(fmax(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                }
+                const bool reach = slab(bb, op, lo, hi);
+                if (COUNT && reach) cnt.tri_tests++;
+                if (!reach) d = -1.0;
+            }
+        }
+        if (mine) atomicAdd(&lr_cnt[oslot], 1u);
+#else
         if (mine) {
             const TriVerts tv = load_tri(VR_TRIS + tri);
             bool reach = true;
@@ -320,6 +364,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             atomicAdd(&lr_cnt[oslot], 1u);
         }
+#endif
         const bool hit = mine && d >= 0.0;
         const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
         if (hit) atomicMin(&lr_d[oslot], bits);
@@ -397,9 +442,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (pr.kind == 0) {
                 ok = plane_distance(pr, pre, dd);
             } else {
-                // the f64 test is skipped only when every lane's line clearly misses the sphere
+                // the f64 test is skipped only when, for every lane, the line clearly misses the
+                // sphere or the sphere lies behind the origin or beyond the lane's best distance
                 // (camera rays of a wave are coherent; so are many bounce rays)
+#if VR_SPHERE_SKIP
+                const float bd = best.kind ? (float)best.d : INFINITY;
+                if (__ballot(!sphere_skip32(pr, pre, bd)) == 0) continue;
+#else
                 if (__ballot(!sphere_missed32(pr, pre)) == 0) continue;
+#endif
                 dd = sphere_distance(pr, pre);
                 ok = dd >= 0.0;
             }
