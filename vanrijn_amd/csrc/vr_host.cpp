@@ -779,12 +779,14 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         // 512 items per atomic keeps the queue counter cold on full frames; a smaller launch would
         // hand 512 items to a few waves and leave the rest of the chip idle at its end (1 spp of
         // 1024^2: 1.9 ms at 512), so every wave gets about 80 slices, in multiples of 64 (one item
-        // per lane).  Measured (1024^2): 256 spp best at 512 (64: +38 %, 256: +0.3 %), 64 spp at
-        // 256 (512: +1.5 %), C5's mesh at 32 spp at 128
+        // per lane), and at least 128: one atomic per 64 items costs more than the tail it saves.
+        // Measured (1024^2): 256 spp best at 512 (64: +38 %, 256: +0.3 %), 64 spp at 256 (512:
+        // +1.5 %), C5's mesh at 32 spp at 128; 512^2 @64 (C2) 128..384 within 2 % (64: +17 %);
+        // 256^2 @16 (C1) flat (profiles/r02/sweeps/sw_grab_*.txt)
         const uint64_t items = ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64 * std::max(1u, p->spp);
         const uint64_t waves = (uint64_t)std::max(1, s->cu_count) * 3 * 4;
         const uint64_t g = items / (waves * 80) / 64 * 64;
-        a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(64, g));
+        a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
     }
     const char* lt = getenv("VR_LEAF_THRESHOLD");  // tuning hooks
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
