@@ -274,7 +274,13 @@ struct RayPre {
     __device__ __forceinline__ bool behind_ok() const { return (flags & 8) != 0; }
 };
 
-__device__ __forceinline__ RayPre prepare(const Ray& r) {
+// the shear constants alone (calculate_shear_to_z_axis, triangle.rs:129-131): begin_ray may
+// defer them to the ray's first BVH entry (only triangle tests and triangle shading read them)
+__device__ __forceinline__ void prepare_shear(RayPre& p) {
+    p.sx = -sel(p.d, p.k0()) / p.pdz;
+    p.sy = -sel(p.d, p.k1()) / p.pdz;
+}
+__device__ __forceinline__ RayPre prepare(const Ray& r, bool shear = true) {
     RayPre p;
     p.o = r.o;
     p.d = r.d;
@@ -285,8 +291,10 @@ __device__ __forceinline__ RayPre prepare(const Ray& r) {
     else rot = (r.d.z > r.d.y) ? 0 : 2;
     const int k0 = rot, k1 = rot == 2 ? 0 : rot + 1, k2 = rot == 0 ? 2 : rot - 1;
     double pdx = sel(r.d, k0), pdy = sel(r.d, k1), pdz = sel(r.d, k2);
-    p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
-    p.sy = -pdy / pdz;
+    if (shear) {
+        p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
+        p.sy = -pdy / pdz;
+    }
     p.pdz = pdz;
     const double tiny = 1e-150;
     const bool exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);

@@ -107,6 +107,9 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_SPHERE_SKIP  // f32 sphere skip: line miss, behind the origin or beyond the best hit
 #define VR_SPHERE_SKIP 0
 #endif
+#ifndef VR_LAZY_SHEAR  // begin_ray: shear constants at the first BVH entry
+#define VR_LAZY_SHEAR 0
+#endif
 #ifndef VR_LATE_BOX  // leaf round: the exact box test only for entries whose triangle hits
 #define VR_LATE_BOX 1
 #endif
@@ -414,6 +417,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 double lo, hi;
                 if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
             }
+            // the ray meets a BVH: its triangle tests need the shear constants (a ray whose wave
+            // meets no BVH skips the two divisions; set again per BVH entry, the same bits)
+            if (VR_LAZY_SHEAR) prepare_shear(pre);
             if (bvh.root4 < 0) {  // a one-triangle BVH
                 test_tri(~bvh.root4);
                 continue;
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // there, not in registers of its own that would stay live through the traversal phase):
     // primitive lists first, then the BVHs
     auto begin_ray = [&]() {
-        pre = prepare(Ray{pre.o, pre.d});
+        pre = prepare(Ray{pre.o, pre.d}, !VR_LAZY_SHEAR);  // shear constants: at the first BVH entry
         pre32 = prepare32(pre, S.extent);
         if (COUNT) cnt.rays++;
         best.kind = kNone;
