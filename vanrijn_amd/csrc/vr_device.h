@@ -43,6 +43,39 @@ __device__ __forceinline__ V3 normalize(V3 a) {  // vec3.rs:103-110 (multiply by
     double inv = 1.0 / sqrt(dot(a, a));
     return mk(a.x * inv, a.y * inv, a.z * inv);
 }
+// normalize for vectors whose squared norm x lies within 4096 spacings of 1.0 (unit vectors
+// rebuilt from unit vectors: a second normalisation, orthonormal-basis transforms, the tangent of
+// two orthogonal unit vectors), with the same bits as normalize.  With u = 2^-52:
+//   x = 1 + k u (k >= 0):      sqrt(x) = 1 + k u/2 - k^2 u^2/8 ...  rounds to s = 1 + floor(k/2) u,
+//                              and 1/s = 1 - j u + j^2 u^2 ...       rounds to 1 - 2j (u/2);
+//   x = 1 - k u/2 (k > 0):     sqrt(x) = 1 - k u/4 - k^2 u^2/32 ... rounds to s = 1 - ceil(k/2) u/2,
+//                              and 1/s = 1 + j u/2 + j^2 u^2/4 ...   rounds to 1 + ceil(j/2) u
+// (the second-order terms are nonzero and far below half a spacing for |k| <= 2^16, so they only
+// break the ties the first-order values sit on).  On the bits: b = bits(x) - bits(1.0) is k above
+// 1 and -k below.  Every such x is checked against the correctly rounded 1 / sqrt(x) in
+// tests/test_normalize_near1.py; other lanes take normalize's sqrt and division.
+#ifndef VR_NEAR1
+#define VR_NEAR1 1
+#endif
+__device__ __forceinline__ V3 normalize_n1(V3 a) {
+#if VR_NEAR1
+    const double x = dot(a, a);
+    const int64_t one = 0x3FF0000000000000ll;
+    const int64_t b = __double_as_longlong(x) - one;
+    double inv;
+    // wave-uniform: the whole wave takes the bit formula or the sqrt and division (a divergent
+    // branch would be if-converted into both)
+    if (__builtin_amdgcn_ballot_w64(!(b >= -4096 && b <= 4096)) == 0) {
+        const int64_t j = b >= 0 ? (b >> 1) : ((1 - b) >> 1);  // s = 1 + j u  or  1 - j u/2
+        inv = __longlong_as_double(b >= 0 ? one - 2 * j : one + ((j + 1) >> 1));
+    } else {
+        inv = 1.0 / sqrt(x);
+    }
+    return mk(a.x * inv, a.y * inv, a.z * inv);
+#else
+    return normalize(a);
+#endif
+}
 __device__ __forceinline__ bool sgn(double x) { return __double_as_longlong(x) < 0; }
 __device__ __forceinline__ double sel(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 __device__ __forceinline__ V3 ldv(const double* p) { return mk(p[0], p[1], p[2]); }
@@ -583,7 +616,7 @@ __device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const Ray
     h.loc = loc;
     h.normal = n;
     h.cotangent = cot;
-    h.tangent = normalize(cross(cot, n));
+    h.tangent = normalize_n1(cross(cot, n));  // cot, n: orthogonal unit vectors
     h.retro = normalize(sub(p.o, loc));
 }
 
@@ -597,7 +630,7 @@ __device__ void prim_info(const Prim& pr, const RayPre& p, double dist, HitInfo&
         h.retro = neg(p.d);
     } else {  // sphere.rs:71-90
         V3 loc = add(p.o, scl(p.d, dist));
-        V3 n = normalize(sub(loc, ldv(pr.vec)));
+        V3 n = normalize_n1(sub(loc, ldv(pr.vec)));  // |loc - c| = r: near 1 for unit spheres
         V3 tan = normalize(cross(n, mk(0.0, 0.0, 1.0)));
         h.loc = loc;
         h.normal = n;

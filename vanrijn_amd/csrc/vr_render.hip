@@ -536,7 +536,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             for (int j = 0; j < S.light_count; ++j) {
                 const V3 ldir = ldv(S.light_dirs + 3 * j);
                 const V3 d1 = normalize(ldir);
-                const RayPre sp = prepare(Ray{add(h.loc, scl(d1, kBounceBias)), normalize(d1)});
+                const RayPre sp = prepare(Ray{add(h.loc, scl(d1, kBounceBias)), normalize_n1(d1)});
                 double term;
                 if (any_hit<STACK>(S, sp, st_node, tid)) {
                     term = material_intensity(&S.materials[S.light_base], lambda);
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const V3 w = mk(x, y, z);
             const double cos_theta = dot(w, mk(0.0, 0.0, 1.0));
             const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-            w_o = normalize(w);
+            w_o = normalize_n1(w);  // |w|^2 = x^2 + y^2 + (1 - x^2 - y^2): 1 within a few spacings
             pdf = (cos_theta * sin_theta) / 3.14159265358979323846;
         }
         // bsdf_to_world = cofactor(M)^T * det (mat3.rs:111-118), applied to w_o by rows
@@ -611,10 +611,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             bsdf_affine(mat, w_i, w_o, lambda, ba, bb);
             Wa = (T * ba) * cosf;
             Wb = (T * bb) * cosf;
-            const V3 d1 = normalize(wo_world);
+            const V3 d1 = normalize_n1(wo_world);  // an orthonormal basis applied to a unit vector
             ++bounces;
             pre.o = add(h.loc, scl(d1, kBounceBias));  // the next ray (state kRayReady)
-            pre.d = normalize(d1);
+            pre.d = normalize_n1(d1);
             state = kRayReady;
             return;
         }
@@ -667,10 +667,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         }
         // Ray::new(location, w_o).bias(1e-7): normalise, step, normalise again (mod.rs:41-61)
         wo_y = wo_world.y;
-        const V3 d1 = normalize(wo_world);
+        const V3 d1 = normalize_n1(wo_world);  // an orthonormal basis applied to a unit vector
         ++bounces;
         pre.o = add(h.loc, scl(d1, kBounceBias));  // the next ray (state kRayReady)
-        pre.d = normalize(d1);
+        pre.d = normalize_n1(d1);
         state = kRayReady;
     };
 
