@@ -599,7 +599,12 @@ __device__ __forceinline__ void triangle_bary(const TriVerts& t, const RayPre& p
 }
 
 // full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96)
-__device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, HitInfo& h) {
+#ifndef VR_RETRO_DIST
+#define VR_RETRO_DIST 0
+#endif
+// `dist`: the hit's distance from triangle_distance, sqrt((o - loc).(o - loc)) over the same loc
+// bits (triangle_bary repeats its operations), so the retro direction's norm is not recomputed
+__device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, double dist, HitInfo& h) {
     double b[3];
     triangle_bary(t, p, b);
     V3 v0 = mk(t.v[0], t.v[1], t.v[2]), v1 = mk(t.v[3], t.v[4], t.v[5]), v2 = mk(t.v[6], t.v[7], t.v[8]);
@@ -617,7 +622,11 @@ __device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const Ray
     h.normal = n;
     h.cotangent = cot;
     h.tangent = normalize_n1(cross(cot, n));  // cot, n: orthogonal unit vectors
+#if VR_RETRO_DIST
+    h.retro = scl(sub(p.o, loc), 1.0 / dist);  // normalize(o - loc): 1 / sqrt(a.a) with sqrt(a.a) == dist
+#else
     h.retro = normalize(sub(p.o, loc));
+#endif
 }
 
 __device__ void prim_info(const Prim& pr, const RayPre& p, double dist, HitInfo& h) {
@@ -864,7 +873,7 @@ __device__ __forceinline__ void hit_info(const DeviceScene& S, const Best& best,
     if (best.kind == kPrim) {
         prim_info(S.prims[best.index], p, best.d, h);
     } else {
-        triangle_info(S.tris[best.index], S.normals[best.index], p, h);
+        triangle_info(S.tris[best.index], S.normals[best.index], p, best.d, h);
         // material of the owning mesh
         int m = 0;
         for (int b = 0; b < S.bvh_count; ++b)
