@@ -107,6 +107,9 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_SPHERE_SKIP  // f32 sphere skip: line miss, behind the origin or beyond the best hit
 #define VR_SPHERE_SKIP 0
 #endif
+#ifndef VR_PLANE_SIGN  // begin_ray: skip the plane division when every lane's plane lies behind it
+#define VR_PLANE_SIGN 0
+#endif
 #ifndef VR_LAZY_SHEAR  // begin_ray: shear constants at the first BVH entry
 #define VR_LAZY_SHEAR 0
 #endif
@@ -446,6 +449,18 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             double dd;
             bool ok;
             if (pr.kind == 0) {
+#if VR_PLANE_SIGN
+                // t = num / dn < 0 whenever num and dn are nonzero with opposite signs (no underflow
+                // to -0 for |num| > 1e-300, |dn| < 1e290): the wave skips the division when that
+                // holds for every lane (bounce rays leaving the plane, upward rays above it)
+                {
+                    const V3 n = ldv(pr.vec);
+                    const double dn = dot(pre.d, n), num = dot(sub(ldv(pr.pre), pre.o), n);
+                    const bool behind = ((num < 0.0 && dn > 0.0) || (num > 0.0 && dn < 0.0)) && fabs(num) > 1e-300 &&
+                                        fabs(dn) < 1e290;
+                    if (__ballot(!behind) == 0) continue;
+                }
+#endif
                 ok = plane_distance(pr, pre, dd);
             } else {
                 // the f64 test is skipped only when, for every lane, the line clearly misses the
