@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 4
+#define VR_ABI_VERSION 5
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -177,8 +177,15 @@ typedef struct vr_scene_info {
     uint64_t device_bytes;   /* scene bytes resident in HBM */
     uint64_t wide_node_count;  /* nodes of the render kernel's 4-wide traversal tree (ABI 3) */
     uint32_t traversal_stack;  /* deepest stack of the 4-wide walk, entries (ABI 3) */
-    uint32_t reserved;
+    uint32_t flags;            /* VR_SCENE_INFO_* (ABI 5) */
 } vr_scene_info;
+/* Every continuation of every path is provably finite (each traced mesh triangle's vertex normals
+ * lie strictly on one side of its plane, so the shading basis of triangle.rs:73-78 is finite at any
+ * barycentric point; no Phong or dielectric material).  Only then does a path whose throughput is
+ * exactly 0 end early; otherwise it is traced to the end, so a later NaN (e.g. the zero normals
+ * mesh.rs:37 gives an OBJ without normals) reaches the pixel as the reference's 0 * NaN does
+ * (simple_random_integrator.rs:39-53). */
+#define VR_SCENE_INFO_NAN_FREE 1u
 int vr_scene_get_info(const vr_scene* scene, vr_scene_info* out);
 /* BVH leaf (in-order) sequence of mesh `mesh`: out[i] = input triangle index of leaf i. */
 int vr_scene_bvh_leaf_order(const vr_scene* scene, uint32_t mesh, uint64_t* out);
@@ -319,6 +326,12 @@ int vr_tone_map(const double* colour_xyz, uint64_t pixel_count, uint8_t* rgb_out
 /* ImageRgbU8::write_png (image.rs:52-66): 8-bit RGB PNG of `height` rows of `width` pixels
  * (row 0 first).  Host only. */
 int vr_write_png(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+
+/* Test hook (no reference counterpart): every hit on scene object `object` takes the singular-
+ * shading-basis path (VR_ERROR_SINGULAR_BASIS, where simple_random_integrator.rs:26-31 panics),
+ * which finite geometry cannot reach; -1 turns it off.  Not thread-safe against concurrent render
+ * calls on the same scene: set it before rendering (tests/test_gpu_concurrency.py).  ABI 5. */
+int vr_debug_set_fault_object(vr_scene* scene, int32_t object);
 
 int vr_device_count(void);
 const char* vr_last_error(void);

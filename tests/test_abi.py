@@ -40,7 +40,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 4
+    assert lib.vr_abi_version() == 5
     assert isinstance(lib.vr_last_error(), bytes)
 
 
@@ -154,3 +154,25 @@ def test_output_buffers_recycle_only_unreferenced_memory():
     c = AccumulationBuffer._for_output(40, 20)  # b's store is free again
     assert c.colour_buffer.ctypes.data == ptr
     assert c.colour_buffer.shape == (20, 40, 3) and c.weight_buffer.shape == (20, 40)
+
+
+def test_output_pool_respects_derived_views():
+    """A slice or reshape of an output array (its numpy .base is the pooled store itself, not the
+    view the pool handed out) keeps the store out of reuse after the buffer is dropped."""
+    import gc
+
+    from vanrijn_amd.render import AccumulationBuffer
+    for derive in (lambda b: b.weight_bias_buffer[:, :], lambda b: b.colour_buffer[..., 0],
+                   lambda b: b.colour_sum_buffer.reshape(-1), lambda b: b.weight_buffer[3:5, 1::2]):
+        a = AccumulationBuffer._for_output(24, 12)
+        kept = derive(a)
+        kept[...] = 7.0
+        del a
+        gc.collect()
+        b = AccumulationBuffer._for_output(24, 12)
+        for arr in (b.colour_buffer, b.colour_sum_buffer, b.colour_bias_buffer, b.weight_buffer, b.weight_bias_buffer):
+            assert not np.shares_memory(arr, kept)
+            arr[...] = -1.0
+        assert (kept == 7.0).all()
+        del b, arr, kept
+        gc.collect()

@@ -8,10 +8,9 @@ call (the reference panics, simple_random_integrator.rs:26-31) must not leak int
 
 det == 0 cannot be produced by finite geometry here (every basis is built from normalised, mutually
 orthogonal vectors; a degenerate one turns into NaN, which the reference does not treat as
-singular either), so the error tests use the library's test hook VR_FAULT_SINGULAR_OBJECT
-(read at scene creation): hits on that object take the singular-basis path.
+singular either), so the error tests use the library's test-only entry point
+vr_debug_set_fault_object: hits on that object take the singular-basis path.
 """
-import os
 import threading
 
 import numpy as np
@@ -83,13 +82,10 @@ def test_eight_threads_partial_render_scene_union(small_main):
 
 @pytest.fixture(scope="module")
 def faulty_scene(small_main, oracle):
-    """The same scene created with the test hook on object 1 (the mesh BVH)."""
-    os.environ["VR_FAULT_SINGULAR_OBJECT"] = "1"
-    try:
-        from vanrijn_amd.scene import DeviceScene
-        ds = DeviceScene(small_main.spec(), 0)
-    finally:
-        del os.environ["VR_FAULT_SINGULAR_OBJECT"]
+    """A second device copy of the scene with the test hook on object 1 (the mesh BVH)."""
+    from vanrijn_amd.scene import DeviceScene
+    ds = DeviceScene(small_main.spec(), 0)
+    ds.set_fault_object(1)
     # rows whose camera rays hit nothing: no shading there, so no fault can occur
     H = W = 64
     ref = oracle.OracleScene(small_main.spec()).render_samples(Tile(0, W, 0, H), H, W, 1, seed=1)

@@ -23,6 +23,7 @@ SCENE_HOST_ONLY = 1
 SCENE_DEVICE_BVH = 2
 SCENE_REFERENCE_BVH = 4
 LAUNCH_TIMED, LAUNCH_COUNTERS = 1, 2
+SCENE_INFO_NAN_FREE = 1
 
 
 class VrError(RuntimeError):
@@ -81,7 +82,7 @@ class SceneDesc(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("triangle_count", C.c_uint64), ("node_count", C.c_uint64), ("max_bvh_depth", C.c_uint32),
                 ("object_count", C.c_uint32), ("extent", C.c_double), ("device_bytes", C.c_uint64),
-                ("wide_node_count", C.c_uint64), ("traversal_stack", C.c_uint32), ("reserved", C.c_uint32)]
+                ("wide_node_count", C.c_uint64), ("traversal_stack", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class TileC(C.Structure):
@@ -147,6 +148,7 @@ SIGNATURES = {
     "vr_tone_map_device": (C.c_int, [_p, _u64, _p, _i32, _p]),
     "vr_tone_map": (C.c_int, [_p, _u64, _p, _i32]),
     "vr_write_png": (C.c_int, [C.c_char_p, _p, _u32, _u32]),
+    "vr_debug_set_fault_object": (C.c_int, [_p, _i32]),
     "vr_device_count": (C.c_int, []),
     "vr_last_error": (C.c_char_p, []),
     "vr_abi_version": (C.c_uint32, []),

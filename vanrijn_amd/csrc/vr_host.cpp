@@ -449,6 +449,11 @@ struct vr_scene {
     std::vector<PendingMesh> pending;
     bool dark0 = true;  // every material's colour(0 nm) == 0: the recursion-limit photon needs no lambda-0 chain
     int mats = 0;       // bit 0: a Lambertian material exists, bit 1: a reflective one
+    // every continuation of every path yields a finite intensity (shading_finite on each traced
+    // mesh, no Phong or dielectric material): then a path with zero throughput may stop early and
+    // the recursion-limit lambda-0 chain may be taken as b0 (DARK0); otherwise both are traced so
+    // that a later NaN reaches the photon as in the reference (0 * NaN)
+    bool nan_free = true;
     // device copies
     void* d_block = nullptr;
     size_t device_bytes = 0;
@@ -467,8 +472,8 @@ struct vr_scene {
     std::unordered_map<void*, int32_t*> stream_slots;
     int cu_count = 0;
     uint64_t partial_seed = 0x5EED0001ull;
-    // test hook (VR_FAULT_SINGULAR_OBJECT at scene creation): hits on this object take the
-    // singular-basis path, which finite geometry cannot reach (DESIGN.md "Errors")
+    // test hook (vr_debug_set_fault_object): hits on this object take the singular-basis path,
+    // which finite geometry cannot reach (DESIGN.md "Errors")
     int32_t fault_object = -1;
 };
 
@@ -590,6 +595,39 @@ static void parallel_copy(void* dst, const void* src, size_t bytes) {
     parallel_range(bytes, (size_t)1 << 20, [&](uint64_t b, uint64_t e) {
         std::memcpy((char*)dst + b, (const char*)src + b, e - b);
     });
+}
+
+// Whether every hit on this mesh has a finite shading basis, whatever the barycentric point: the
+// reference's normal = normalize(sum b_i N_i) (triangle.rs:73-78) is NaN where the interpolated
+// normal is zero (mesh.rs:37 gives zero normals to an OBJ without them), and cotangent =
+// normalize((V0 - V1) x n) is NaN where n is parallel to that edge.  Sufficient: all three vertex
+// normals lie strictly on one side of the triangle's plane, by a relative margin of 1e-6 (then
+// n . f >= 1e-6 |N|max |f| sum(b) - O(1e-16), so n is nonzero and not in the plane, where the edge
+// lies), with magnitudes far from f64 under- / overflow.  Degenerate triangles fail.  (A sphere's
+// basis is NaN only where a hit's x and y equal the centre's exactly, and a retro direction only
+// where a hit lies exactly at the ray origin: exact-equality events of measure zero, not excluded.)
+static bool shading_finite(const vr_mesh_desc& m) {
+    for (uint64_t t = 0; t < m.triangle_count; ++t) {
+        const double* v = m.vertices + 9 * t;
+        const double* nn = m.normals + 9 * t;
+        for (int i = 0; i < 9; ++i)
+            if (!std::isfinite(v[i]) || !std::isfinite(nn[i]) || std::fabs(v[i]) > 1e100 || std::fabs(nn[i]) > 1e100)
+                return false;
+        const double e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        const double f[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const double fl = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+        if (!(fl > 1e-200)) return false;
+        double nmax = 0.0, d[3];
+        for (int k = 0; k < 3; ++k) {
+            const double* n = nn + 3 * k;
+            nmax = std::max(nmax, std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]));
+            d[k] = n[0] * f[0] + n[1] * f[1] + n[2] * f[2];
+        }
+        if (!(nmax > 1e-100)) return false;
+        const double m6 = 1e-6 * nmax * fl;
+        if (!((d[0] > m6 && d[1] > m6 && d[2] > m6) || (d[0] < -m6 && d[1] < -m6 && d[2] < -m6))) return false;
+    }
+    return true;
 }
 
 // spectrum.rs:64-79's sample wavelengths as the reference computes them (before / after), and the
@@ -766,6 +804,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
     const char* sm = getenv("VR_SHADE_MIN");  // tuning hook: defer shading below this many hits
     a.shade_min = sm ? (uint32_t)std::max(0, atoi(sm)) : 16u;
+    a.early_stop = s->nan_free ? 1u : 0u;
+    if (const char* es = getenv("VR_EARLY_STOP")) a.early_stop = atoi(es) != 0 && s->nan_free;  // A/B hook (off only)
     const char* mm = getenv("VR_MISS_MIN");  // tuning hook: defer finishing misses
     a.miss_min = mm ? (uint32_t)std::max(0, atoi(mm)) : 8u;
     const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
@@ -1003,7 +1043,6 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     if (!s) return fail(VR_ERROR_OUT_OF_MEMORY, "scene allocation failed");
     s->device = device;
     s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
-    if (const char* fo = getenv("VR_FAULT_SINGULAR_OBJECT")) s->fault_object = (int32_t)atoi(fo);
     s->camera[0] = desc->camera_location.x;
     s->camera[1] = desc->camera_location.y;
     s->camera[2] = desc->camera_location.z;
@@ -1124,6 +1163,14 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
         }
     }
     s->object_count = desc->object_count;
+    // NaN-capable continuations (shading_finite): no early stop, the general lambda-0 chain
+    if (s->mats & 4) s->nan_free = false;
+    for (uint32_t mi = 0; mi < desc->mesh_count && s->nan_free; ++mi) {
+        const vr_mesh_desc& m = desc->meshes[mi];
+        if (mesh_object[mi] >= 0 && m.triangle_count && m.vertices && m.normals && !shading_finite(m))
+            s->nan_free = false;
+    }
+    if (!s->nan_free) s->dark0 = false;
     s->leaf_order.resize(desc->mesh_count);
     s->mesh_tri_base.assign(desc->mesh_count, 0);
     // device build: requested, a device exists for it, and no NaN coordinate (the reference's
@@ -1297,7 +1344,13 @@ int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     out->device_bytes = s->device_bytes;
     out->wide_node_count = s->wide_count;
     out->traversal_stack = (uint32_t)s->wide_stack;
-    out->reserved = 0;
+    out->flags = s->nan_free ? VR_SCENE_INFO_NAN_FREE : 0u;
+    return VR_OK;
+}
+
+int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
+    if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
+    s->fault_object = object < 0 ? -1 : object;
     return VR_OK;
 }
 
@@ -1338,6 +1391,24 @@ struct PassEvents {
     }
 };
 
+// Records the context's `done` on the call's stream when it goes out of scope, so that EVERY exit of
+// a call after its first enqueue -- an error return included -- orders the context's next user
+// (possibly on another stream) after the work this call left queued on its staging, mask, queue
+// counter and scratch.  (The success paths record `done` themselves as well: recording it again
+// at the same point of the stream changes nothing.)
+struct DoneOnExit {
+    hipEvent_t done;
+    hipStream_t st;
+    ~DoneOnExit() { (void)hipEventRecord(done, st); }
+};
+
+// persistent grid: workgroups per CU of the render kernel (3: 3 waves per SIMD); VR_GRID_PER_CU
+// overrides (diagnostic: throughput against occupancy)
+int grid_per_cu() {
+    static const int per_cu = getenv("VR_GRID_PER_CU") ? std::max(1, atoi(getenv("VR_GRID_PER_CU"))) : 3;
+    return per_cu;
+}
+
 int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* state, hipStream_t st, int32_t* err,
                    bool counting, bool recording, void* records, unsigned long long* counters,
                    unsigned long long* wg_times, PassEvents* timing = nullptr) {
@@ -1359,6 +1430,7 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         return fail(VR_ERROR_UNSUPPORTED, "too many pixel blocks x samples in one launch (2^32)");
     // the context's previous user (possibly on another stream) must be done with its buffers
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    DoneOnExit guard{c->done, st};
     int rc = ctx_grow(&c->staging, &c->staging_bytes, (size_t)(16 * npix * pass), c->done);
     if (rc) return rc;
     // blocks whose camera rays all miss every object (one small kernel per call; VR_BLOCK_CULL=0
@@ -1396,11 +1468,8 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         }
         // LDS stack entries: the 4-wide walk's, and the binary walk's for Whitted shadow rays
         const int stack = s->dev.integrator == 1 ? std::max(stack_depth(s), wide_stack_depth(s)) : wide_stack_depth(s);
-        // persistent grid: 3 workgroups per CU (3 waves per SIMD); VR_GRID_PER_CU overrides
-        // (diagnostic: throughput against occupancy)
-        static const int per_cu = getenv("VR_GRID_PER_CU") ? std::max(1, atoi(getenv("VR_GRID_PER_CU"))) : 3;
         int lr = vr::launch_render(a, stack, counting, recording, s->dark0, s->mats ? s->mats : 3,
-                                   std::max(1, s->cu_count) * per_cu, st, mid);
+                                   std::max(1, s->cu_count) * grid_per_cu(), st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {
             hipEvent_t end = timing->add();
@@ -1442,7 +1511,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     // diagnostic (tools): with counters, VR_WG_TIMES_PATH receives per-workgroup start/end stamps
     const char* wg_path = counting ? getenv("VR_WG_TIMES_PATH") : nullptr;
     CallScratch wg;
-    const uint64_t blocks = (uint64_t)std::max(1, s->cu_count) * 3;  // persistent grid limit
+    const uint64_t blocks = (uint64_t)std::max(1, s->cu_count) * grid_per_cu();  // persistent grid limit
     unsigned long long* counters = nullptr;
     if (counting) {
         lock.lock();
@@ -1543,6 +1612,7 @@ int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation
     CallCtx* c = L.c;
     const hipStream_t st = c->stream;
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    DoneOnExit guard{c->done, st};
     double *state = nullptr, *planar = nullptr;
     rc = host_call_scratch(c, n, 0, &state, &planar, nullptr);
     if (rc) return rc;
@@ -1648,6 +1718,7 @@ int vr_render_samples(const vr_scene* s, const vr_render_params* p, vr_sample_re
     CallCtx* c = L.c;
     const hipStream_t st = c->stream;
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    DoneOnExit guard{c->done, st};
     const size_t rec_bytes = n * p->spp * sizeof(vr_sample_record);
     double* state = nullptr;
     void* rec = nullptr;
@@ -1676,6 +1747,7 @@ int vr_trace_rays(const vr_scene* s, uint64_t n, const double* origins, const do
     CallCtx* c = L.c;
     const hipStream_t st = c->stream;
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
+    DoneOnExit guard{c->done, st};
     const size_t in_bytes = n * 3 * sizeof(double), out_bytes = n * sizeof(vr_hit_record);
     rc = ctx_grow(&c->scratch, &c->scratch_bytes, 2 * in_bytes + out_bytes, c->done);
     if (rc) return rc;

@@ -145,6 +145,10 @@ struct RenderArgs {
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
+    // 1: a path whose throughput and affine term are both 0 ends early (its intensity is 0 for
+    // every continuation) -- set only for scenes whose continuations are provably finite
+    // (vr_host.cpp shading_finite); 0: traced to the end like the reference, so 0 * NaN stays NaN
+    uint32_t early_stop;
     // ImageSampler film constants (camera.rs:24-66): film_w * (1 / width), film_w * 0.5,
     // film_h * (1 / height), film_h * 0.5 -- the kernel's expressions, evaluated once
     double film[4];

@@ -119,6 +119,9 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
+#ifndef VR_STAGE_NT  // staged photons written with the non-temporal hint (A/B: plain stores)
+#define VR_STAGE_NT 1
+#endif
 constexpr int kWaveList = 64 * kPend;
 // room for a node step's leaves: per lane (at most kPend queued per lane), or -- VR_WAVE_CAP --
 // for the wave (the FIFO has room for a step of all 64 lanes: any one lane may queue more)
@@ -502,8 +505,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
         // streamed once to HBM and read once by the reduce: non-temporal, so the 16 B per sample
         // (4.3 GB per 1024^2 x 256 frame) do not evict the BVH and triangles from L2 and MALL
+#if VR_STAGE_NT
         __builtin_nontemporal_store(wl, &out[0]);
         __builtin_nontemporal_store(I, &out[1]);
+#else
+        out[0] = wl;
+        out[1] = I;
+#endif
         if (RECORD) {
             const double Is = I * 360.0;
             const V3 c = xyz_for_wavelength(wl);
@@ -675,8 +683,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             Acc0 = Acc0 + T0 * bterm;
             T0 = T0 * a0;
         }
+        // A path whose every continuation yields intensity 0 stops here -- only in scenes the host
+        // proved NaN-free (A.early_stop: every mesh triangle's shading basis is finite for any
+        // barycentric point, no Phong / dielectric): the reference keeps recursing and returns
+        // inner x 0, which is NaN when a later bounce is (simple_random_integrator.rs:39-53).
         const bool zero_tail = DARK0 ? (b0 == 0.0) : (T0 == 0.0 && Acc0 == 0.0);
-        if (!RECORD && T == 0.0 && Acc == 0.0 && zero_tail) {
+        if (!RECORD && A.early_stop && T == 0.0 && Acc == 0.0 && zero_tail) {
             finish(lambda, 0.0);  // every continuation yields intensity 0
             return;
         }
@@ -739,7 +751,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     depth += 1;
                     if (depth == kRecursionLimit) {  // integrate(.., 0) returns {0, 0}: lambda becomes 0
                         flags |= 2;
-                        finish(0.0, DARK0 ? b0 : Acc0);
+                        // the innermost photon's intensity 0 times the lambda-0 throughput: + 0
+                        // when finite, NaN when a level's pdf * |cos| was (the reference's 0 * NaN);
+                        // DARK0 scenes are NaN-free (host), where every lambda-0 level is 0 * I + b
+                        finish(0.0, DARK0 ? b0 : Acc0 + T0 * 0.0);
                     } else {
                         go = true;
                     }

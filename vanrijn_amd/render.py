@@ -9,8 +9,8 @@
 Every render call goes through the C ABI into the gfx950 kernels; nothing here computes a pixel.
 """
 import ctypes as C
+import sys
 import threading
-import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -63,13 +63,14 @@ class TileIterator:
 
 class _OutputPool:
     """Backing stores for output AccumulationBuffers (11 f64 per pixel).  A store is handed out
-    again only when every view made from it has been garbage-collected (weak references), so a
-    caller holding any array of an old buffer keeps its memory to itself."""
+    again only when nothing but the pool refers to it: every numpy view derived from a store --
+    the five arrays of a buffer, and any slice or reshape a caller makes of them -- holds the store
+    itself as its `.base`, so the store's reference count says whether any such view is alive."""
 
     def __init__(self, keep=32):
         self.keep = keep
         self.lock = threading.Lock()
-        self.stores = []  # [backing array, [weakref per view]]
+        self.stores = []  # backing arrays
 
     @staticmethod
     def _split(store, width, height):
@@ -78,26 +79,26 @@ class _OutputPool:
                 store[6 * n:9 * n].reshape(height, width, 3), store[9 * n:10 * n].reshape(height, width),
                 store[10 * n:11 * n].reshape(height, width))
 
+    def _free(self, i):
+        # references: the pool's list and getrefcount's own argument; any live view adds its .base
+        return sys.getrefcount(self.stores[i]) <= 2
+
     def views(self, width, height):
         size = 11 * width * height
         with self.lock:
-            for entry in self.stores:
-                if entry[0].size == size and all(r() is None for r in entry[1]):
-                    vs = self._split(entry[0], width, height)
-                    entry[1] = [weakref.ref(v) for v in vs]
-                    return vs
-        store = np.empty(size)
-        vs = self._split(store, width, height)
-        with self.lock:
-            self.stores.append([store, [weakref.ref(v) for v in vs]])
-            if len(self.stores) > self.keep:  # drop a free store (or the oldest record of one)
-                for i, e in enumerate(self.stores):
-                    if all(r() is None for r in e[1]):
+            for i in range(len(self.stores)):
+                if self.stores[i].size == size and self._free(i):
+                    return self._split(self.stores[i], width, height)
+            store = np.empty(size)
+            self.stores.append(store)
+            if len(self.stores) > self.keep:  # forget a free store (or the oldest: its views keep it alive)
+                for i in range(len(self.stores)):
+                    if self._free(i):
                         del self.stores[i]
                         break
                 else:
                     del self.stores[0]
-        return vs
+            return self._split(store, width, height)
 
 
 _OUTPUT_POOL = _OutputPool()

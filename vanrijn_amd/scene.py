@@ -365,7 +365,14 @@ class DeviceScene:
     def info(self):
         i = N.SceneInfo()
         N.check(N.lib().vr_scene_get_info(self.handle, C.byref(i)))
-        return {n: getattr(i, n) for n, _ in i._fields_}
+        d = {n: getattr(i, n) for n, _ in i._fields_}
+        d["nan_free"] = bool(d["flags"] & N.SCENE_INFO_NAN_FREE)
+        return d
+
+    def set_fault_object(self, obj):
+        """Test hook (vr_debug_set_fault_object): hits on scene object `obj` report the singular
+        shading basis (VR_ERROR_SINGULAR_BASIS); -1 turns it off."""
+        N.check(N.lib().vr_debug_set_fault_object(self.handle, obj))
 
     NODE_DTYPE = np.dtype([("box", "<f8", (2, 6)), ("child", "<i4", (2,)), ("pad", "<i4", (6,))])
 
