@@ -10,18 +10,23 @@ Workload (default --config c3 = BASELINE.json configs[2] / metric): the main.rs 
 the deterministic procedural stand-in (69,312 triangles, vanrijn_amd/scenes.py).  One "step" = one
 frame: rank r renders sample indices [(step*N + r)*spp, +spp) of the same image (weak scaling for
 c1-c3; c4 / c5 split ONE frame's 1024 / 256 spp over the N ranks, strong scaling), then the
-per-pixel accumulation records (8 f64) are summed onto rank 0 with one RCCL reduce over xGMI inside
+per-pixel sums {X, Y, Z, weight} (32 B) are summed onto rank 0 with one RCCL reduce over xGMI inside
 the timed region (vanrijn_amd/distributed.py frame_step, the same step the gloo tests run).
 
 Printed (rank 0, one JSON line):
   value       total samples of all ranks / max-over-ranks wall time of the timed steps;
-  roofline    the render kernel against its binding ceiling.  The bound and its fraction come from
-              the rocprofv3 PMC record of this exact library build and config (profiles/
-              pmc_records.json, tools/pmc.sh + tools/pmc_summary.py): VALU issue (f64-heavy vector
-              ALU) vs HBM.  `achieved` = VALU issue cycles per launch (PMC instruction mix x issue
-              cost) / the live HIP-event kernel time; `hbm_frac` = PMC HBM bytes / kernel time / 8 TB/s;
-              SURVEY.md 8(d)'s algorithmic-bytes formula is kept as `algorithmic_*` (its bytes are
-              served by L2 / MALL, not HBM, so its fraction is no physical bound);
+  roofline    the render kernel against its binding ceiling, from rocprofv3 PMC passes run by this
+              bench itself on this build and workload (live_pmc: child processes, one counter group
+              each; the committed profiles/pmc_records.json only if they fail): VALU issue (f64-heavy
+              vector ALU) vs HBM.  `achieved` = VALU issue cycles per launch (the PMC instruction
+              mix x the issue cost of each class measured by tools/opcost.hip, profiles/r03/
+              opcost.json) / the live HIP-event kernel time; `hbm_frac` = PMC HBM bytes (2 FETCH_SIZE
+              + WRITE_SIZE) / kernel time / 8 TB/s; SURVEY.md 8(d)'s algorithmic-bytes formula is
+              kept as `algorithmic_*` (its bytes are served by L2 / MALL, not HBM, so its fraction is
+              no physical bound); lane utilisation and per-launch counters come from a counting
+              launch of the same workload and need no PMC;
+  scene_build vr_scene_create time (excluded from `value`, SURVEY.md 8(d));
+  reduce      bytes and RCCL time per step of the cross-GPU reduce;
   drop_in     the reference's own call pattern (src/main.rs:197-216): host threads each calling
               vr_partial_render_scene for 1-spp full frames into host AccumulationBuffers, merged
               by vr_merge_tile on the main thread (N = 1, rank 0);
@@ -72,11 +77,48 @@ BYTES_PER_TRI_TEST = 72
 BYTES_PER_SHADED_TRI = 72
 BYTES_PER_PIXEL_STATE = 32
 
-# Issue cost of one wave64 VALU instruction on a gfx950 SIMD, in cycles (MI355X_MICROARCH.md:
-# wave64 f32 VALU over 2 cycles; f64 FMA/ADD/MUL at half the f32 rate (78.6 vs 157.3 TF spec);
-# f64 transcendentals (rcp/rsq/sqrt) taken at a quarter of the f64 rate).  Other f64 opcodes
-# (div_scale/fmas/fixup, compares, min/max) are counted at the f32 cost: a lower bound.
-VALU_CYCLES = {"other": 2, "f64": 4, "trans_f64": 16}
+# Issue cost of one wave64 VALU instruction on a gfx950 SIMD, in cycles, MEASURED by
+# tools/opcost.hip (profiles/r03/opcost.json): SIMD busy cycles per instruction with 3 waves per
+# SIMD -- the render kernel's occupancy -- each issuing independent instructions of one opcode.
+# Every rocprofv3 instruction class is priced by its representative opcodes; the remainder of
+# SQ_INSTS_VALU (moves, selects, compares, logic, bit-field ops) by the median of those opcodes.
+OPCOST_PATH = os.path.join(ROOT, "profiles", "r03", "opcost.json")
+OCCUPANCY_WAVES_PER_SIMD = 3
+PMC_CLASS_OPCODES = {
+    "SQ_INSTS_VALU_FMA_F64": ["v_fma_f64", "v_div_fmas_f64"],
+    "SQ_INSTS_VALU_ADD_F64": ["v_add_f64"],
+    "SQ_INSTS_VALU_MUL_F64": ["v_mul_f64"],
+    "SQ_INSTS_VALU_TRANS_F64": ["v_rcp_f64", "v_sqrt_f64", "v_rsq_f64"],
+    "SQ_INSTS_VALU_INT64": ["v_lshlrev_b64", "v_mad_u64_u32"],
+    "SQ_INSTS_VALU_INT32": ["v_add_u32", "v_mul_lo_u32", "v_bfe_u32"],
+    "SQ_INSTS_VALU_FMA_F32": ["v_fma_f32", "v_pk_fma_f32"],
+    "SQ_INSTS_VALU_ADD_F32": ["v_add_f32"],
+    "SQ_INSTS_VALU_MUL_F32": ["v_add_f32"],
+    "SQ_INSTS_VALU_TRANS_F32": None,  # not measured: MI355X_MICROARCH.md's 8 cycles (v_exp_f32 ...)
+    "SQ_INSTS_VALU_CVT": ["v_cvt_f64_i32", "v_cvt_f32_f64"],
+}
+OTHER_OPCODES = ["v_mov_b32", "v_xor_b32", "v_cndmask_b32_e64 (sgpr mask)", "v_cmp_lt_f32", "v_cmp_lt_u32",
+                 "v_cmp_lt_f64", "v_max_f32", "v_max_f64", "v_min_f64", "v_div_scale_f64", "v_div_fixup_f64"]
+
+
+def issue_costs():
+    """Cycles per instruction per PMC class from the committed microbenchmark (None if absent)."""
+    try:
+        rows = json.load(open(OPCOST_PATH))["results"]
+    except (OSError, ValueError, KeyError):
+        return None
+    cpi = {r["op"]: r["cycles_per_inst"] for r in rows if r["waves_per_simd"] == OCCUPANCY_WAVES_PER_SIMD}
+
+    def mean(ops):
+        v = [cpi[o] for o in ops if o in cpi]
+        return sum(v) / len(v) if v else None
+
+    costs = {k: (mean(v) if v else 8.0) for k, v in PMC_CLASS_OPCODES.items()}
+    other = sorted(cpi[o] for o in OTHER_OPCODES if o in cpi)
+    costs["other"] = other[len(other) // 2] if other else None
+    if any(v is None for v in costs.values()):
+        return None
+    return costs
 
 
 def algorithmic_bytes(c, pixels):
@@ -114,17 +156,95 @@ def pmc_record(key):
     return rec
 
 
-def valu_issue_cycles(pmc):
-    f64 = pmc["SQ_INSTS_VALU_FMA_F64"] + pmc["SQ_INSTS_VALU_ADD_F64"] + pmc["SQ_INSTS_VALU_MUL_F64"]
-    trans = pmc["SQ_INSTS_VALU_TRANS_F64"]
-    other = pmc["SQ_INSTS_VALU"] - f64 - trans
-    return VALU_CYCLES["other"] * other + VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans
+def valu_issue_cycles(pmc, costs):
+    classified = sum(pmc[k] for k in PMC_CLASS_OPCODES)
+    return sum(pmc[k] * costs[k] for k in PMC_CLASS_OPCODES) + (pmc["SQ_INSTS_VALU"] - classified) * costs["other"]
 
 
-def roofline(counts, pixels, kernel_s, key, passes=1):
+# ---------------------------------------------------------------------------- live PMC (rocprofv3)
+# One counter group per rocprofv3 run, --kernel-trace beside --pmc only (MI355X_MICROARCH.md), each
+# pass a child process (bench.py --pmc-child: the same workload, one timed frame) under its own time
+# limit; nothing here runs under the profiler itself.
+PMC_PASSES = [
+    ("fetch", ["FETCH_SIZE"]),
+    ("write", ["WRITE_SIZE"]),
+    ("mix1", ["SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+              "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_CVT"]),
+    ("mix2", ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
+              "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "SQ_WAVES"]),
+    ("tcc", ["TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE"]),
+]
+
+
+def _is_timed_render(name):
+    # render_kernel<STACK, COUNT, RECORD, ...>: the timed launches have COUNT = false, RECORD = false
+    if "render_kernel<" not in name:
+        return False
+    targs = name.split("render_kernel<")[1].split(">")[0].split(",")
+    return targs[1].strip() == "false" and targs[2].strip() == "false"
+
+
+def _fold_pass(d):
+    import csv
+    per, dur = {}, {}
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if _is_timed_render(r["Kernel_Name"]):
+            x = per.setdefault(int(r["Dispatch_Id"]), {})
+            x[r["Counter_Name"]] = x.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    tr = os.path.join(d, "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        for r in csv.DictReader(open(tr)):
+            if _is_timed_render(r["Kernel_Name"]):
+                dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    last = max(per)
+    return per[last], dur.get(last)
+
+
+def live_pmc(child_args, timeout_s=150):
+    """Run the PMC passes on this build and workload; returns a record like profiles/pmc_records.json's
+    (per_launch counters, kernel_ns) or {"error": ...}."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return {"error": "rocprofv3 not found"}
+    tmp = tempfile.mkdtemp(prefix="vr_pmc_")
+    per_launch, kernel_ns = {}, {}
+    try:
+        for name, counters in PMC_PASSES:
+            d = os.path.join(tmp, name)
+            cmd = [prof, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--pmc"] + counters + \
+                  ["--", sys.executable, os.path.abspath(__file__), "--pmc-child"] + child_args
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True,
+                                 env=dict(os.environ, TMPDIR=tmp))
+            try:
+                rc = p.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return {"error": f"PMC pass {name} exceeded {timeout_s} s"}
+            if rc != 0:
+                return {"error": f"PMC pass {name} exited {rc}"}
+            c, ns = _fold_pass(d)
+            per_launch.update(c)
+            if ns:
+                kernel_ns[name] = ns
+    except (OSError, ValueError, KeyError) as e:
+        return {"error": f"PMC passes: {e}"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {"per_launch": per_launch, "kernel_ns": kernel_ns.get("tcc") or max(kernel_ns.values()),
+            "kernel_ns_per_pass": kernel_ns, "lib_sha256": lib_sha(),
+            "source": "live: rocprofv3 --pmc passes of this run's build and workload (bench.py live_pmc)"}
+
+
+def roofline(counts, pixels, kernel_s, key, passes=1, pmc=None):
     """kernel_s: the render kernel's time per step (all its launches: a frame whose staging exceeds
     the per-launch cap runs in `passes` equal launches); the PMC record holds one launch, so its
-    rates use the per-launch time kernel_s / passes."""
+    rates use the per-launch time kernel_s / passes.  `pmc`: this run's live PMC record, else the
+    committed record of this library build (profiles/pmc_records.json)."""
     alg = algorithmic_bytes(counts, pixels)
     r = {"kernel": "render_kernel", "kernel_ms": round(kernel_s * 1e3, 3), "launches_per_step": passes,
          "algorithmic_bytes_per_launch": alg,
@@ -137,16 +257,18 @@ def roofline(counts, pixels, kernel_s, key, passes=1):
                                                         "path_loop_slots", "exact_box_tests")},
          "traversal_lane_utilisation": round(counts["node_visits"] / max(1, counts["traversal_slots"]), 4),
          "path_loop_lane_utilisation": round(counts["rays"] / max(1, counts["path_loop_slots"]), 4)}
-    rec = pmc_record(key)
-    if rec is None:
+    rec = pmc if pmc and "per_launch" in pmc else pmc_record(key)
+    costs = issue_costs()
+    if rec is None or costs is None:
+        why = (pmc or {}).get("error") or f"no PMC record for this library build on '{key}' (tools/pmc.sh)"
         r.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                  "pmc": f"no PMC record for this library build on '{key}' (tools/pmc.sh)"})
+                  "pmc": why if rec is None else "no opcode cost table (profiles/r03/opcost.json)"})
         return r
     pmc = rec["per_launch"]
     launch_s = kernel_s / max(1, passes)
     traffic = 2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024  # gfx950: FETCH_SIZE counts 128-B lines at 64 B
     hbm_gbs = traffic / launch_s / 1e9
-    valu = valu_issue_cycles(pmc)
+    valu = valu_issue_cycles(pmc, costs)
     valu_rate = valu / launch_s / 1e9  # G SIMD-cycles of VALU issue per second
     valu_peak = SIMDS * CLOCK_GHZ
     clk = pmc["GRBM_GUI_ACTIVE"] / 8 / (rec["kernel_ns"] * 1e-9) / 1e9  # effective clock of the profiled launch
@@ -161,17 +283,20 @@ def roofline(counts, pixels, kernel_s, key, passes=1):
         "traffic": traffic,
         "hbm_gbs": round(hbm_gbs, 2), "hbm_frac": round(fracs["hbm"], 4),
         "valu_issue_frac": round(fracs["valu"], 4),
-        "valu_issue_cycles_per_launch": valu, "valu_cost_model_cycles": VALU_CYCLES,
+        # the same issue cycles against the profiled launch's own clock (DVFS holds it below 2.4 GHz)
+        "valu_issue_frac_at_profiled_clock": round(valu / (rec["kernel_ns"] * 1e-9) / (SIMDS * clk * 1e9), 4),
+        "valu_issue_cycles_per_launch": valu,
+        "valu_cost_model_cycles": {k: round(v, 3) for k, v in costs.items()},
+        "valu_cost_source": os.path.relpath(OPCOST_PATH, ROOT) + " (tools/opcost.hip, 3 waves/SIMD)",
         "valu_insts_per_launch": pmc["SQ_INSTS_VALU"],
         "f64_insts_per_launch": pmc["SQ_INSTS_VALU_FMA_F64"] + pmc["SQ_INSTS_VALU_ADD_F64"] +
         pmc["SQ_INSTS_VALU_MUL_F64"] + pmc["SQ_INSTS_VALU_TRANS_F64"],
-        # rocprof's gfx94x VALUBusy formula (ACTIVE_INST_VALU quad-cycles x 4 / SIMDs / cycles): it sums
-        # per-wave busy time, so waves interleaving on one SIMD count twice -- an upper bound
-        "valu_busy_pmc": round(pmc["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / (pmc["GRBM_GUI_ACTIVE"] / 8), 4),
-        "wave_wait_any_frac": round(pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"], 4),
+        "wave_wait_any_frac": round(pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"], 4)
+        if pmc.get("SQ_WAVE_CYCLES") else None,
         "l2_hit_rate": round(pmc["TCC_HIT_sum"] / (pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"]), 4)
         if "TCC_HIT_sum" in pmc else None,
         "profiled_clock_ghz": round(clk, 3),
+        "profiled_kernel_ms": round(rec["kernel_ns"] / 1e6, 3),
         "pmc": rec.get("source"),
     })
     return r
@@ -298,7 +423,11 @@ def main():
     ap.add_argument("--drop-in-frames", type=int, default=64)
     ap.add_argument("--drop-in-threads", type=int, default=8)
     ap.add_argument("--no-drop-in", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes of the roofline")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
     args = ap.parse_args()
+    if args.pmc_child:
+        args.steps, args.warmup, args.no_drop_in, args.no_cpu_baseline, args.no_pmc = 1, 0, True, True, True
 
     cfg = dict(CONFIGS[args.config])
     for k in ("width", "height", "spp", "scene"):
@@ -322,18 +451,34 @@ def main():
         scene = scenes.synthetic_scene()
     else:
         scene = scenes.main_scene(args.mesh) if cfg["scene"] == "main" else scenes.bench_scene(args.mesh)
+    # scene build (excluded from the metric, reported separately): vr_scene_create of
+    # the default traversal tree (host median-split reference tree for the tie ranks + binned-SAH
+    # tree + 4-wide collapse + upload), and of the reference tree built on the device
+    t_build = time.perf_counter()
     dscene = scene.device_scene(local)
     info = dscene.info()
+    build_s = time.perf_counter() - t_build
+    build = {"default_tree_s": round(build_s, 4), "default_tree": "host: median-split ranks + binned SAH + 4-wide"}
+    if not args.pmc_child:
+        t_build = time.perf_counter()
+        scene.device_scene(local, device_bvh=True).info()
+        build["device_reference_tree_s"] = round(time.perf_counter() - t_build, 4)
     tile = Tile(0, W, 0, H)
     state = torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}")
     stream = torch.cuda.current_stream()
+
+    reduce_events = []
 
     def step(i, timed=False):
         def shard(first, st):
             return render_tile_device(dscene, tile, H, W, spp, SEED, first, st.data_ptr(), stream.cuda_stream,
                                       timed=timed, device=local)
-        return D.frame_step(shard, state, i, spp)
+        return D.frame_step(shard, state, i, spp, timer=reduce_events if timed else None)
 
+    if args.pmc_child:  # under rocprofv3 (live_pmc): one timed frame of the workload, nothing else
+        step(1, timed=True)
+        torch.cuda.synchronize()
+        return
     # counting launch (untimed): traversal counters of exactly this workload
     counts = render_tile_device(dscene, tile, H, W, spp, SEED, rank * spp, state.data_ptr(), stream.cuda_stream,
                                 counters=True, device=local)
@@ -361,6 +506,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    rccl_ms = [a.elapsed_time(b) for a, b in reduce_events]
     samples = world * args.steps * W * H * spp
     value = samples / elapsed / 1e6
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -390,8 +536,19 @@ def main():
                    "triangles": info["triangle_count"], "bvh_depth": info["max_bvh_depth"],
                    "parallelism": f"spp-split x{world}, RCCL reduce",
                    "pmc_key": config_key(cfg["scene"], W, H, spp)},
-        "roofline": roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes)),
     }
+    pmc = None
+    if rank == 0 and world == 1 and not args.no_pmc:
+        child = ["--config", args.config, "--width", str(W), "--height", str(H), "--spp", str(cfg["spp"]),
+                 "--scene", cfg["scene"]] + (["--mesh", args.mesh] if args.mesh else [])
+        pmc = live_pmc(child)
+    out["roofline"] = roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes), pmc)
+    out["scene_build"] = build
+    # the path's one exchange: {sum X, Y, Z, weight} of every pixel, 32 B, reduced
+    # onto rank 0 inside the timed step (RCCL; under torch.distributed.run also at world size 1)
+    out["reduce"] = {"collective": "dist.reduce(SUM, f64) onto rank 0" if distributed else "none (one process)",
+                     "bytes_per_step_per_rank": D.reduce_bytes(state) if distributed else 0,
+                     "ms_per_step": round(sum(rccl_ms) / len(rccl_ms), 3) if rccl_ms else 0.0}
     out["roofline"]["reduce_kernel_ms"] = round(sum(reduce_ms) / len(reduce_ms), 3)
     # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied
     # as the photon {0, 0} without tracing: the records are bit-identical with VR_BLOCK_CULL=0

@@ -119,3 +119,34 @@ def test_shard_spp():
 def test_reduce_is_a_no_op_on_one_process():
     s = torch.arange(16, dtype=torch.float64)
     assert torch.equal(D.reduce_records(s.clone()), s)  # no process group: nothing reduced or zeroed
+
+
+def test_reduce_moves_only_the_sums():
+    """32 B per pixel -- {sum X, sum Y, sum Z, weight} -- not the whole 64-B record."""
+    state = torch.zeros(H * W * 8, dtype=torch.float64)
+    assert D.reduce_bytes(state) == 32 * H * W
+    assert D.SUMS == (0, 1, 2, 6) and sorted(D.SUMS + D.BIAS_COLUMNS) == list(range(8))
+
+
+def _keep_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rec = torch.arange(5 * 8, dtype=torch.float64).reshape(5, 8) + 100 * rank
+    mine = rec.clone()
+    D.reduce_records(rec.view(-1))
+    if rank == 0:
+        want = sum(torch.arange(5 * 8, dtype=torch.float64).reshape(5, 8) + 100 * r for r in range(world))
+        want[:, 3:6] = 0.0
+        want[:, 7] = 0.0
+        assert torch.equal(rec, want)
+    else:
+        assert torch.equal(rec, mine)  # a non-destination rank keeps its own records
+    np.save(f"{out_path}.{rank}.npy", rec.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reduce_destination_and_other_ranks(tmp_path):
+    out = str(tmp_path / "keep")
+    mp.spawn(_keep_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert all(os.path.exists(f"{out}.{r}.npy") for r in range(3))

@@ -6,7 +6,10 @@
 // 64-bit integer and compare / select opcodes the kernel issues (tools/isa_sections.py's static
 // mix) the same way: each wave runs a loop of 32 independent instructions of one opcode (8
 // accumulators x 4), and the SIMD's cycles per instruction are
-//     (wave lifetime in shader cycles, s_memtime) / (instructions per wave x waves sharing the SIMD).
+//     (the SIMD's busy span in shader cycles: first wave start .. last wave end, s_memtime)
+//     / (instructions per wave x waves sharing the SIMD),
+// the median over the chip's SIMDs (a wave's own lifetime undercounts when the waves of a SIMD do
+// not start together).
 // Occupancy is forced by LDS: a 256-thread workgroup (4 waves, one per SIMD) reserves 96 / 64 /
 // 48 / 36 KB, so exactly 1 / 2 / 3 / 4 workgroups fit a CU's 160 KB, and the grid is that many
 // workgroups per CU; every wave also records its hardware id (CU, SIMD, XCC), and the host checks
@@ -38,13 +41,15 @@
 enum Op {
     kAddF64, kMulF64, kFmaF64, kMaxF64, kMinF64, kRcpF64, kSqrtF64, kRsqF64, kDivScaleF64, kDivFmasF64,
     kDivFixupF64, kCmpF64, kFractF64, kLdexpF64, kCvtF64I32, kCvtF32F64, kAddF32, kFmaF32, kPkFmaF32,
-    kCndmask, kAddU32, kMulLoU32, kLshl64, kMadU64U32, kAdd64, kBfeU32, kNumOps
+    kCndmask, kAddU32, kMulLoU32, kLshl64, kMadU64U32, kAdd64, kBfeU32, kCndmaskE64, kMovB32, kXorB32,
+    kMaxF32, kCmpF32, kCmpU32, kNumOps
 };
 static const char* kNames[kNumOps] = {
     "v_add_f64", "v_mul_f64", "v_fma_f64", "v_max_f64", "v_min_f64", "v_rcp_f64", "v_sqrt_f64", "v_rsq_f64",
     "v_div_scale_f64", "v_div_fmas_f64", "v_div_fixup_f64", "v_cmp_lt_f64", "v_fract_f64", "v_ldexp_f64",
     "v_cvt_f64_i32", "v_cvt_f32_f64", "v_add_f32", "v_fma_f32", "v_pk_fma_f32", "v_cndmask_b32", "v_add_u32",
-    "v_mul_lo_u32", "v_lshlrev_b64", "v_mad_u64_u32", "v_add_co_u32+v_addc_co_u32 (one 64-bit add)", "v_bfe_u32"};
+    "v_mul_lo_u32", "v_lshlrev_b64", "v_mad_u64_u32", "v_add_co_u32+v_addc_co_u32 (one 64-bit add)", "v_bfe_u32",
+    "v_cndmask_b32_e64 (sgpr mask)", "v_mov_b32", "v_xor_b32", "v_max_f32", "v_cmp_lt_f32", "v_cmp_lt_u32"};
 
 template <int OP>
 __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned (&w)[8],
@@ -157,6 +162,30 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
 #define ASM_U(i) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(u[i]));
         D8(ASM_U)
 #undef ASM_U
+    } else if constexpr (OP == kCndmaskE64) {
+#define ASM_S(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u[i]) : "v"(ub), "s"(0x5555555555555555ull));
+        D8(ASM_S)
+#undef ASM_S
+    } else if constexpr (OP == kMovB32) {
+#define ASM_U(i) asm volatile("v_mov_b32 %0, %1" : "=v"(u[i]) : "v"(w[i]));
+        D8(ASM_U)
+#undef ASM_U
+    } else if constexpr (OP == kXorB32) {
+#define ASM_U(i) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        D8(ASM_U)
+#undef ASM_U
+    } else if constexpr (OP == kMaxF32) {
+#define ASM_F(i) asm volatile("v_max_f32 %0, %0, %1" : "+v"(f[i]) : "v"(fb));
+        D8(ASM_F)
+#undef ASM_F
+    } else if constexpr (OP == kCmpF32) {
+#define ASM_C(i) asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(q[i]) : "v"(f[i]), "v"(fb));
+        D8(ASM_C)
+#undef ASM_C
+    } else if constexpr (OP == kCmpU32) {
+#define ASM_C(i) asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(q[i]) : "v"(u[i]), "v"(ub));
+        D8(ASM_C)
+#undef ASM_C
     }
 #undef ASM_D
 }
@@ -194,9 +223,10 @@ __global__ __launch_bounds__(256) void opk(int iters, unsigned long long* out, d
     for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i] + (double)w[i] + (double)q[i];
     sink[blockIdx.x * 256 + tid] = acc;  // keeps every result live
     if ((tid & 63) == 0) {
-        unsigned long long* o = out + 4 * (blockIdx.x * 4 + (tid >> 6));
-        o[0] = t1 - t0;
-        o[1] = r1 - r0;
+        unsigned long long* o = out + 5 * (blockIdx.x * 4 + (tid >> 6));
+        o[0] = t0;
+        o[1] = t1;
+        o[4] = r1 - r0;
         o[2] = hw;
         o[3] = xcc;
     }
@@ -227,9 +257,9 @@ int main(int argc, char** argv) {
     const int max_grid = cus * 4;
     unsigned long long* d_out = nullptr;
     double* d_sink = nullptr;
-    CHECK(hipMalloc(&d_out, sizeof(unsigned long long) * 4 * 4 * max_grid));
+    CHECK(hipMalloc(&d_out, sizeof(unsigned long long) * 5 * 4 * max_grid));
     CHECK(hipMalloc(&d_sink, sizeof(double) * 256 * max_grid));
-    std::vector<unsigned long long> h(4 * 4 * max_grid);
+    std::vector<unsigned long long> h(5 * 4 * max_grid);
     std::printf("{\"device_cus\": %d, \"iters\": %d, \"insts_per_wave\": %d, \"results\": [\n", cus, iters, iters * 32);
     bool first = true;
     for (int op = 0; op < kNumOps; ++op) {
@@ -239,31 +269,37 @@ int main(int argc, char** argv) {
             CHECK(hipDeviceSynchronize());
             launch_op(op, k, grid, iters, d_out, d_sink);
             CHECK(hipDeviceSynchronize());
-            CHECK(hipMemcpy(h.data(), d_out, sizeof(unsigned long long) * 4 * 4 * grid, hipMemcpyDeviceToHost));
-            // waves per SIMD from the hardware ids: (xcc, se, cu, simd) -> count
-            std::map<std::tuple<unsigned, unsigned, unsigned, unsigned>, int> per_simd;
-            std::vector<double> cyc, clk;
+            CHECK(hipMemcpy(h.data(), d_out, sizeof(unsigned long long) * 5 * 4 * grid, hipMemcpyDeviceToHost));
+            // per SIMD (xcc, se, cu, simd from the hardware ids): its waves and busy span
+            std::map<std::tuple<unsigned, unsigned, unsigned, unsigned>, std::vector<int>> per_simd;
+            std::vector<double> life, clk;
             for (int w = 0; w < 4 * grid; ++w) {
-                const unsigned long long* o = &h[4 * w];
+                const unsigned long long* o = &h[5 * w];
                 const unsigned hw = (unsigned)o[2], xcc = (unsigned)o[3] & 0xf;
-                per_simd[std::make_tuple(xcc, (hw >> 13) & 7, (hw >> 8) & 15, (hw >> 4) & 3)]++;
-                cyc.push_back((double)o[0]);
-                clk.push_back((double)o[0] / ((double)o[1] / 100.0));  // MHz: memrealtime ticks at 100 MHz
+                per_simd[std::make_tuple(xcc, (hw >> 13) & 7, (hw >> 8) & 15, (hw >> 4) & 3)].push_back(w);
+                life.push_back((double)(o[1] - o[0]));
+                clk.push_back((double)(o[1] - o[0]) / ((double)o[4] / 100.0));  // MHz (memrealtime: 100 MHz)
             }
             int lo = 1 << 30, hi = 0;
+            std::vector<double> cpi;
             for (auto& kv : per_simd) {
-                lo = std::min(lo, kv.second);
-                hi = std::max(hi, kv.second);
+                lo = std::min(lo, (int)kv.second.size());
+                hi = std::max(hi, (int)kv.second.size());
+                unsigned long long t0 = ~0ull, t1 = 0;
+                for (int w : kv.second) {
+                    t0 = std::min(t0, h[5 * w]);
+                    t1 = std::max(t1, h[5 * w + 1]);
+                }
+                cpi.push_back((double)(t1 - t0) / ((double)iters * 32.0 * (double)kv.second.size()));
             }
-            std::sort(cyc.begin(), cyc.end());
+            std::sort(cpi.begin(), cpi.end());
+            std::sort(life.begin(), life.end());
             std::sort(clk.begin(), clk.end());
-            const double med = cyc[cyc.size() / 2];
-            const double per_inst = med / ((double)iters * 32.0 * k);
             std::printf("%s  {\"op\": \"%s\", \"waves_per_simd\": %d, \"simds\": %zu, \"waves_per_simd_min\": %d, "
-                        "\"waves_per_simd_max\": %d, \"cycles_per_inst\": %.3f, \"wave_cycles_min\": %.0f, "
-                        "\"wave_cycles_median\": %.0f, \"wave_cycles_max\": %.0f, \"clock_mhz_median\": %.0f}",
-                        first ? "" : ",\n", kNames[op], k, per_simd.size(), lo, hi, per_inst, cyc.front(), med,
-                        cyc.back(), clk[clk.size() / 2]);
+                        "\"waves_per_simd_max\": %d, \"cycles_per_inst\": %.3f, \"cycles_per_inst_p10\": %.3f, "
+                        "\"cycles_per_inst_p90\": %.3f, \"wave_lifetime_median\": %.0f, \"clock_mhz_median\": %.0f}",
+                        first ? "" : ",\n", kNames[op], k, per_simd.size(), lo, hi, cpi[cpi.size() / 2],
+                        cpi[cpi.size() / 10], cpi[cpi.size() * 9 / 10], life[life.size() / 2], clk[clk.size() / 2]);
             first = false;
         }
     }

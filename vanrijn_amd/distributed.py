@@ -15,6 +15,7 @@ import torch
 import torch.distributed as dist
 
 RECORD = 8  # f64 per pixel
+SUMS = (0, 1, 2, 6)  # the merge-exact part of a record: sum X, Y, Z and the weight (32 B per pixel)
 BIAS_COLUMNS = (3, 4, 5, 7)  # Kahan compensations of the XYZ sums and of the weight
 
 
@@ -40,19 +41,37 @@ def shard_spp(total_spp, world, split):
     return total_spp // world
 
 
-def reduce_records(state: torch.Tensor, dst=0, group=None):
+def reduce_bytes(state: torch.Tensor):
+    """Bytes one rank contributes to the reduce: the 4 f64 sums of every pixel."""
+    return state.numel() // RECORD * len(SUMS) * state.element_size()
+
+
+def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None):
     """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path).
 
-    The summed Kahan compensations belong to no single update_pixel sequence
-    (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
-    reduced state then starts a fresh compensated sum from the merged totals."""
+    Only the merge-exact sums {sum X, sum Y, sum Z, weight} travel -- 32 B per pixel, half the
+    record: they are gathered into one packed buffer, reduced, and scattered back on `dst`.  The
+    Kahan compensations belong to no single update_pixel sequence once sums of different ranks are
+    added (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
+    reduced state starts a fresh compensated sum from the merged totals.  Other ranks keep their
+    own records.  `timer`: a list that receives (start, end) CUDA events around the collective."""
     rank, world = world_info(group)
     # through the collective whenever a group exists (at world size 1 too: bench.py under
     # torch.distributed.run on one GPU rehearses the RCCL step the 8-GPU runs take)
     if dist.is_available() and dist.is_initialized():
-        dist.reduce(state, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        s = state.view(-1, RECORD)
+        cols = torch.tensor(SUMS, device=state.device)
+        packed = s.index_select(1, cols)  # [pixels][4], contiguous
+        ev = None
+        if timer is not None and state.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        dist.reduce(packed, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if ev is not None:
+            ev[1].record()
+            timer.append(ev)
         if rank == dst:
-            s = state.view(-1, RECORD)
+            s.index_copy_(1, cols, packed)
             s[:, 3:6] = 0.0
             s[:, 7] = 0.0
     return state
@@ -65,11 +84,11 @@ def mean_colour(state: torch.Tensor):
     return torch.where(w != 0, s[:, 0:3] * (1.0 / w), torch.zeros_like(s[:, 0:3]))
 
 
-def frame_step(render_shard, state: torch.Tensor, step, spp, group=None):
+def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=None):
     """One frame on this rank: render_shard(first_sample, state) renders (or enqueues) this rank's
     `spp` samples per pixel into `state` (fresh records), then the records are reduced onto rank 0.
     Returns what render_shard returned (launch stats on the GPU)."""
     rank, world = world_info(group)
     out = render_shard(first_sample(step, rank, world, spp), state)
-    reduce_records(state, group=group)
+    reduce_records(state, group=group, timer=timer)
     return out
