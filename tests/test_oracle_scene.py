@@ -144,3 +144,24 @@ def test_oracle_accumulate_continuation(oracle, small_mesh):
                           accumulate={k: v for k, v in two.items() if k != "counters"})
     for k in ("colour", "colour_sum", "colour_bias", "weight", "weight_bias"):
         assert np.array_equal(once[k], two[k])
+
+
+@pytest.mark.slow
+def test_pruned_render_equals_exhaustive_c5_mesh(oracle):
+    """C5's 1,051,392-triangle mesh (the deep tree the full-frame C5 GPU test compares against the
+    pruned mode): on a crop of the 4096^2 frame through the mesh's silhouette, and on rays that
+    enter the mesh region from everywhere, the pruned mode's closest hits and every sample's
+    decisions and intensity are the reference mode's."""
+    scene = scenes.synthetic_scene()
+    orc = oracle.OracleScene(scene.spec())
+    # inside the mesh's disc, and across its left silhouette (the plane behind it)
+    for t in (Tile(1700, 1740, 2200, 2240), Tile(1086, 1126, 3110, 3150)):
+        a = orc.render_samples(t, 4096, 4096, 2, seed=0x5EED0001, mode=oracle.MODE_REFERENCE, nthreads=8)
+        b = orc.render_samples(t, 4096, 4096, 2, seed=0x5EED0001, mode=oracle.MODE_PRUNED, nthreads=8)
+        assert (a["flags"] & 1).sum() > 1000
+        for k in ("bounces", "flags", "wavelength", "intensity"):
+            assert np.array_equal(a[k], b[k]), k
+    o, d = _rays(scene.spec(), 3000, 17)
+    ref, _ = orc.trace(o, d, oracle.MODE_REFERENCE)
+    prn, _ = orc.trace(o, d, oracle.MODE_PRUNED)
+    _same_hits(ref, prn)

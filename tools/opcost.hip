@@ -42,14 +42,15 @@ enum Op {
     kAddF64, kMulF64, kFmaF64, kMaxF64, kMinF64, kRcpF64, kSqrtF64, kRsqF64, kDivScaleF64, kDivFmasF64,
     kDivFixupF64, kCmpF64, kFractF64, kLdexpF64, kCvtF64I32, kCvtF32F64, kAddF32, kFmaF32, kPkFmaF32,
     kCndmask, kAddU32, kMulLoU32, kLshl64, kMadU64U32, kAdd64, kBfeU32, kCndmaskE64, kMovB32, kXorB32,
-    kMaxF32, kCmpF32, kCmpU32, kNumOps
+    kMaxF32, kCmpF32, kCmpU32, kMulF32, kCndmaskE64Vcc, kCndmaskSaluVcc, kNumOps
 };
 static const char* kNames[kNumOps] = {
     "v_add_f64", "v_mul_f64", "v_fma_f64", "v_max_f64", "v_min_f64", "v_rcp_f64", "v_sqrt_f64", "v_rsq_f64",
     "v_div_scale_f64", "v_div_fmas_f64", "v_div_fixup_f64", "v_cmp_lt_f64", "v_fract_f64", "v_ldexp_f64",
     "v_cvt_f64_i32", "v_cvt_f32_f64", "v_add_f32", "v_fma_f32", "v_pk_fma_f32", "v_cndmask_b32", "v_add_u32",
     "v_mul_lo_u32", "v_lshlrev_b64", "v_mad_u64_u32", "v_add_co_u32+v_addc_co_u32 (one 64-bit add)", "v_bfe_u32",
-    "v_cndmask_b32_e64 (sgpr mask)", "v_mov_b32", "v_xor_b32", "v_max_f32", "v_cmp_lt_f32", "v_cmp_lt_u32"};
+    "v_cndmask_b32_e64 (sgpr mask)", "v_mov_b32", "v_xor_b32", "v_max_f32", "v_cmp_lt_f32", "v_cmp_lt_u32", "v_mul_f32",
+    "v_cndmask_b32_e64 (vcc operand)", "v_cndmask_b32 (vcc from s_mov_b64)"};
 
 template <int OP>
 __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned (&w)[8],
@@ -186,6 +187,20 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
 #define ASM_C(i) asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(q[i]) : "v"(u[i]), "v"(ub));
         D8(ASM_C)
 #undef ASM_C
+    } else if constexpr (OP == kMulF32) {
+#define ASM_F(i) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f[i]) : "v"(fb));
+        D8(ASM_F)
+#undef ASM_F
+    } else if constexpr (OP == kCndmaskE64Vcc) {
+#define ASM_S(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
+        D8(ASM_S)
+#undef ASM_S
+    } else if constexpr (OP == kCndmaskSaluVcc) {
+        // vcc written by the scalar unit (no VALU-written lane mask in flight)
+        asm volatile("s_mov_b64 vcc, 0x5555" ::: "vcc");
+#define ASM_S(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
+        D8(ASM_S)
+#undef ASM_S
     }
 #undef ASM_D
 }
