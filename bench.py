@@ -113,11 +113,13 @@ def issue_costs():
         v = [cpi[o] for o in ops if o in cpi]
         return sum(v) / len(v) if v else None
 
-    costs = {k: (mean(v) if v else 8.0) for k, v in PMC_CLASS_OPCODES.items()}
     other = sorted(cpi[o] for o in OTHER_OPCODES if o in cpi)
-    costs["other"] = other[len(other) // 2] if other else None
-    if any(v is None for v in costs.values()):
+    if not other:
         return None
+    costs = {"other": other[len(other) // 2]}
+    for k, v in PMC_CLASS_OPCODES.items():
+        # a class without a measured opcode: TRANS_F32 at the guide's 8 cycles, else "other"
+        costs[k] = (mean(v) if v else None) or (8.0 if v is None else costs["other"])
     return costs
 
 

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -42,7 +43,8 @@ enum Op {
     kAddF64, kMulF64, kFmaF64, kMaxF64, kMinF64, kRcpF64, kSqrtF64, kRsqF64, kDivScaleF64, kDivFmasF64,
     kDivFixupF64, kCmpF64, kFractF64, kLdexpF64, kCvtF64I32, kCvtF32F64, kAddF32, kFmaF32, kPkFmaF32,
     kCndmask, kAddU32, kMulLoU32, kLshl64, kMadU64U32, kAdd64, kBfeU32, kCndmaskE64, kMovB32, kXorB32,
-    kMaxF32, kCmpF32, kCmpU32, kMulF32, kCndmaskE64Vcc, kCndmaskSaluVcc, kNumOps
+    kMaxF32, kCmpF32, kCmpU32, kMulF32, kCndmaskE64Vcc, kCndmaskSaluVcc, kCndmaskE32Fresh, kFmacF64,
+    kCndmaskE32Mixed, kNumOps
 };
 static const char* kNames[kNumOps] = {
     "v_add_f64", "v_mul_f64", "v_fma_f64", "v_max_f64", "v_min_f64", "v_rcp_f64", "v_sqrt_f64", "v_rsq_f64",
@@ -50,7 +52,8 @@ static const char* kNames[kNumOps] = {
     "v_cvt_f64_i32", "v_cvt_f32_f64", "v_add_f32", "v_fma_f32", "v_pk_fma_f32", "v_cndmask_b32", "v_add_u32",
     "v_mul_lo_u32", "v_lshlrev_b64", "v_mad_u64_u32", "v_add_co_u32+v_addc_co_u32 (one 64-bit add)", "v_bfe_u32",
     "v_cndmask_b32_e64 (sgpr mask)", "v_mov_b32", "v_xor_b32", "v_max_f32", "v_cmp_lt_f32", "v_cmp_lt_u32", "v_mul_f32",
-    "v_cndmask_b32_e64 (vcc operand)", "v_cndmask_b32 (vcc from s_mov_b64)"};
+    "v_cndmask_b32_e64 (vcc operand)", "v_cndmask_b32 (vcc from s_mov_b64)", "v_cndmask_b32 (e32, fresh destination)",
+    "v_fmac_f64", "v_cndmask_b32 (e32) + v_add_u32 interleaved (pair)"};
 
 template <int OP>
 __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned (&w)[8],
@@ -201,6 +204,18 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
 #define ASM_S(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
         D8(ASM_S)
 #undef ASM_S
+    } else if constexpr (OP == kCndmaskE32Fresh) {
+#define ASM_S(i) asm volatile("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(u[i]) : "v"(w[i]), "v"(ub));
+        D8(ASM_S)
+#undef ASM_S
+    } else if constexpr (OP == kFmacF64) {
+#define ASM_D2(i) asm volatile("v_fmac_f64 %0, %1, %1" : "+v"(d[i]) : "v"(db));
+        D8(ASM_D2)
+#undef ASM_D2
+    } else if constexpr (OP == kCndmaskE32Mixed) {
+#define ASM_S(i) asm volatile("v_cndmask_b32 %0, %0, %2, vcc\n\tv_add_u32 %1, %1, %2" : "+v"(u[i]), "+v"(w[i]) : "v"(ub));
+        D8(ASM_S)
+#undef ASM_S
     }
 #undef ASM_D
 }
@@ -267,6 +282,7 @@ static void launch_op(int op, int k, int grid, int iters, unsigned long long* ou
 
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2048;
+    const char* only = argc > 2 ? argv[2] : nullptr;  // substring filter on the opcode names
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int max_grid = cus * 4;
@@ -278,6 +294,7 @@ int main(int argc, char** argv) {
     std::printf("{\"device_cus\": %d, \"iters\": %d, \"insts_per_wave\": %d, \"results\": [\n", cus, iters, iters * 32);
     bool first = true;
     for (int op = 0; op < kNumOps; ++op) {
+        if (only && !std::strstr(kNames[op], only)) continue;
         for (int k = 1; k <= 4; ++k) {
             const int grid = cus * k;
             launch_op(op, k, grid, iters / 8, d_out, d_sink);  // warm-up (clocks, code fetch)

@@ -799,6 +799,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.wg_times = nullptr;
     a.error_flag = nullptr;  // per call (enqueue_passes)
     a.block_mask = nullptr;  // per call (enqueue_passes)
+    a.live_blocks = nullptr;
+    a.live_count = nullptr;
     a.fault_object = s->fault_object;
     const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
@@ -832,6 +834,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = getenv("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
+    const char* lf = getenv("VR_LEAF_FEW");  // tuning hook (0: off)
+    a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {
@@ -1437,13 +1441,22 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
     // turns the test off)
     const bool cull = !(getenv("VR_BLOCK_CULL") && atoi(getenv("VR_BLOCK_CULL")) == 0);
     const uint8_t* mask = nullptr;
+    const uint32_t *live = nullptr, *live_count = nullptr;
     if (cull && !recording) {  // (the record variant writes every sample's record)
-        rc = ctx_grow(&c->mask, &c->mask_bytes, (size_t)(((tw + 7) / 8) * ((th + 7) / 8)), c->done);
+        // mask: 1 B per block; then the live-block list (4 B per block) and its count (16-B aligned)
+        const uint64_t nb = ((tw + 7) / 8) * ((th + 7) / 8);
+        const size_t list_off = (nb + 15) & ~(uint64_t)15;
+        rc = ctx_grow(&c->mask, &c->mask_bytes, (size_t)(list_off + 4 * nb + 16), c->done);
         if (rc) return rc;
+        if (nb >= (1ull << 32)) return fail(VR_ERROR_UNSUPPORTED, "too many pixel blocks in one tile (2^32)");
         vr::RenderArgs a = make_args(s, p, state);
-        const int lc = vr::launch_block_cull(a, (uint8_t*)c->mask, st);
+        int lc = vr::launch_block_cull(a, (uint8_t*)c->mask, st);
+        uint32_t* lst = (uint32_t*)((char*)c->mask + list_off);
+        if (!lc) lc = vr::launch_block_compact((const uint8_t*)c->mask, (uint32_t)nb, lst, lst + nb, st);
         if (lc) return fail(VR_ERROR_DEVICE, vr::device_error_string(lc));
         mask = (const uint8_t*)c->mask;
+        live = lst;
+        live_count = lst + nb;
     }
     for (uint64_t done = 0; done < p->spp; done += pass) {
         vr_render_params q = *p;
@@ -1455,6 +1468,8 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         a.queue = c->queue;
         a.error_flag = err;
         a.block_mask = mask;
+        a.live_blocks = live;
+        a.live_count = live_count;
         a.records = records;
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;

@@ -142,6 +142,7 @@ struct RenderArgs {
     uint32_t grab;                // items a wave takes from the queue per atomic (0: exactly its need)
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
+    uint32_t leaf_few;            // ... or at most this many lanes are still traversing
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
@@ -165,6 +166,11 @@ struct RenderArgs {
     // per 8x8 pixel block of the tile: 1 when every camera ray through the block provably misses
     // every object (block_cull_kernel), so each of its samples is photon {0, 0}; nullptr: none
     const uint8_t* block_mask;
+    // the tile's 8x8 blocks that are NOT culled, in block order (block_compact_kernel), and their
+    // count: work items enumerate only these, so culled blocks cost the work queue nothing;
+    // nullptr: every block of the tile is live
+    const uint32_t* live_blocks;
+    const uint32_t* live_count;
 };
 
 struct TraceArgs {
@@ -200,6 +206,8 @@ int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool r
 // vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
 // the camera-frustum test of every 8x8 block of a launch's tile into mask (RenderArgs::block_mask)
 int launch_block_cull(const RenderArgs& args, uint8_t* mask, void* stream);
+// the live (unculled) blocks of `mask` (n blocks) in order into live[], their number into *count
+int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32_t* count, void* stream);
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
 // vr_image.hip: device records (8 f64 per pixel) <-> the host AccumulationBuffer's five arrays laid
 // out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read;

@@ -207,7 +207,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     uint32_t samples_done = 0;
     if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
-    const uint64_t per_chunk = (uint64_t)bw * bh * 64;
+    // work items run over the live blocks only (frustum-culled blocks are not in the item space)
+    const uint32_t nlive = A.live_blocks ? __builtin_amdgcn_readfirstlane(*A.live_count) : bw * bh;
+    const double rcp_live = A.live_blocks ? 1.0 / (double)nlive : A.rcp_blocks;
+    const uint64_t per_chunk = (uint64_t)nlive * 64;
     const uint64_t items = render_items(A, per_chunk);
     const uint64_t rounds = chunk_rounds(A);
     const uint32_t bulk = A.spp - tail_of(A);
@@ -799,20 +802,20 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         // a launch's items), quotients by f64 reciprocal, corrected by one
                         const uint32_t gb = (uint32_t)(g >> 6), l = (uint32_t)(g & 63);
                         const uint32_t nblk = (uint32_t)(per_chunk >> 6);
-                        uint32_t chunk_i = (uint32_t)((double)gb * A.rcp_blocks);
+                        uint32_t chunk_i = (uint32_t)((double)gb * rcp_live);
                         int32_t rem = (int32_t)(gb - chunk_i * nblk);
                         if (rem < 0) { --chunk_i; rem += (int32_t)nblk; }
                         if (rem >= (int32_t)nblk) { ++chunk_i; rem -= (int32_t)nblk; }
-                        const uint32_t blk = (uint32_t)rem;
+                        const uint32_t blk = A.live_blocks ? A.live_blocks[rem] : (uint32_t)rem;
                         uint32_t by = (uint32_t)((double)blk * A.rcp_bw);
                         int32_t bx = (int32_t)(blk - by * bw);
                         if (bx < 0) { --by; bx += (int32_t)bw; }
                         if (bx >= (int32_t)bw) { ++by; bx -= (int32_t)bw; }
                         const uint32_t x = (uint32_t)bx * 8 + (l & 7), y = by * 8 + (l >> 3);
-                        // else padding, or a block whose camera rays all miss every object (its
-                        // samples are the photon {0, 0}: the ordered reduce applies them without
-                        // staged data): take another item
-                        if (x < A.tile_width && y < A.tile_height && !(kargs()->block_mask && kargs()->block_mask[blk])) {
+                        // else padding: take another item (blocks whose camera rays all miss every
+                        // object are not in the item space; their samples are the photon {0, 0},
+                        // applied by the ordered reduce without staged data)
+                        if (x < A.tile_width && y < A.tile_height) {
                             px = x;
                             py = y;
                             if (chunk_i < rounds) {
@@ -968,7 +971,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const uint32_t queued = q_tail - q_head;
             if (queued != 0) {
                 const bool stalled = np > 0 && (node < 0 || !(VR_ROOM));
-                if (queued >= A.leaf_threshold || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
+                // few lanes still traversing (a launch's tail, a long path alone in its wave): test
+                // their leaves at once, so the hits found tighten the distance cull of the rest of
+                // the walk -- waiting for a full round would walk the whole tree unculled
+                const bool few = __popcll(__ballot(state == kTraversing)) <= (int)A.leaf_few;
+                if (queued >= A.leaf_threshold || few || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
                     __ballot(state == kTraversing && node >= 0 && VR_ROOM) == 0) {
                     VR_SEC(0);
                     VR_MARK("leaf_test");
@@ -1127,6 +1134,29 @@ __global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Pri
         clear = sphere_clear(c, 0.5 * sqrt(dot(e, e)) * (1.0 + 1e-9) + 1e-12);
     }
     mask[b] = clear ? 1 : 0;
+}
+
+// The live blocks of a cull mask in block order (one workgroup: each thread counts a contiguous
+// run of blocks, an LDS scan gives the runs' offsets, then each thread writes its run's live ones).
+__global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask, uint32_t n, uint32_t* live,
+                                                              uint32_t* count) {
+    __shared__ uint32_t part[1024];
+    const uint32_t tid = threadIdx.x, per = (n + 1023) / 1024;
+    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i) c += mask[i] == 0;
+    part[tid] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+        const uint32_t v = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t off = part[tid] - c;
+    for (uint32_t i = lo; i < hi; ++i)
+        if (mask[i] == 0) live[off++] = i;
+    if (tid == 1023) *count = part[1023];
 }
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -1336,6 +1366,11 @@ int launch_block_cull(const RenderArgs& a, uint8_t* mask, void* stream) {
     if (blocks == 0) return 0;
     hipLaunchKernelGGL(dev::block_cull_kernel, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        a, a.scene.prims, a.scene.bvhs, mask);
+    return (int)hipGetLastError();
+}
+
+int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32_t* count, void* stream) {
+    hipLaunchKernelGGL(dev::block_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, n, live, count);
     return (int)hipGetLastError();
 }
 
