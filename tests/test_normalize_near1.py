@@ -41,3 +41,31 @@ def test_normalised_vectors_land_in_the_range():
     got = u * inv_norm_near1(b)[:, None]
     want = u * (1.0 / np.sqrt(x))[:, None]
     assert np.array_equal(got, want)
+
+
+def half_recip_near1(b):
+    """vr_device.h half_recip_near1: b = bits(a) - bits(1.0) -> bits of 1.0 / (2.0 * a)."""
+    b = np.asarray(b, dtype=np.int64)
+    r = np.where(b >= 0, ONE - 2 * b, ONE + ((1 - b) >> 1))
+    return 0.5 * r.view(np.float64)
+
+
+def test_sphere_half_reciprocal_bitwise():
+    """Sphere::intersect's one_over_2_a = 1.0 / (2.0 * a) (sphere.rs:65), a = d.d of a normalised
+    direction: every a the kernel's range admits (and 16x more) against IEEE division."""
+    b = np.arange(-65536, 65537, dtype=np.int64)
+    a = (ONE + b).view(np.float64)
+    want = 1.0 / (2.0 * a)
+    got = half_recip_near1(b)
+    assert np.array_equal(got.view(np.int64), want.view(np.int64)), b[got != want][:8]
+
+
+def test_sphere_a_of_normalised_directions_lands_in_the_range():
+    """a = ((0 + dx dx) + dy dy) + dz dz (sphere.rs:43-47, fold from 0.0) of the kernel's ray
+    directions (normalize / normalize_n1 of arbitrary vectors) lies within a few spacings of 1."""
+    rng = np.random.default_rng(9)
+    v = rng.normal(size=(200_000, 3)) * rng.uniform(1e-3, 1e3, size=(200_000, 1))
+    inv = 1.0 / np.sqrt(((-0.0 + v[:, 0] * v[:, 0]) + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2])
+    d = v * inv[:, None]
+    a = ((0.0 + d[:, 0] * d[:, 0]) + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    assert np.abs(a.view(np.int64) - ONE).max() <= 16

@@ -480,13 +480,33 @@ __device__ __forceinline__ double triangle_distance(const TriVerts& t, const Ray
     return sqrt(dot(dv, dv));
 }
 
-// Sphere::intersect (sphere.rs:39-93), decision part: distance or -1
-__device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p) {
-    V3 o = p.o, d = p.d, c = ldv(s.vec);
+// sphere.rs:43-47's a = sum of d * d (fold from 0.0) -- the same for every sphere a ray meets
+__device__ __forceinline__ double sphere_a(V3 d) {
     double a = 0.0;
     a = a + d.x * d.x;
     a = a + d.y * d.y;
     a = a + d.z * d.z;
+    return a;
+}
+// 1.0 / (2.0 * a) (sphere.rs:65) for a near 1 (every ray direction here is normalised, so a lies
+// within a few spacings of 1), with the bits of the division: 2a is exact and RN(1 / 2a) =
+// RN(1 / a) / 2.  With u = 2^-52 and b = bits(a) - bits(1.0):
+//   a = 1 + b u (b >= 0):      1 / a = 1 - b u + b^2 u^2 ...   rounds to 1 - 2b (u/2): bits(1.0) - 2b;
+//   a = 1 - k u/2 (k = -b > 0): 1 / a = 1 + k u/2 + k^2 u^2/4 ... rounds to 1 + ceil(k/2) u
+// (the second-order terms are positive and far below half a spacing for |b| <= 4096: they only
+// break the tie an odd k sits on, upward).  Checked against IEEE division for every such a in
+// tests/test_normalize_near1.py; a wave with any other a divides.
+__device__ __forceinline__ double half_recip_near1(double a) {
+    const int64_t one = 0x3FF0000000000000ll;
+    const int64_t b = __double_as_longlong(a) - one;
+    if (__builtin_amdgcn_ballot_w64(!(b >= -4096 && b <= 4096)) == 0)
+        return 0.5 * __longlong_as_double(b >= 0 ? one - 2 * b : one + ((1 - b) >> 1));
+    return 1.0 / (2.0 * a);
+}
+// Sphere::intersect (sphere.rs:39-93), decision part: distance or -1; `a` = sphere_a(p.d) and
+// `one_over_2_a` = 1 / (2a) of the ray, hoisted out of the loop over spheres (the same bits)
+__device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p, double a, double one_over_2_a) {
+    V3 o = p.o, d = p.d, c = ldv(s.vec);
     V3 bv = scl(sub(mk(o.x * d.x, o.y * d.y, o.z * d.z), mk(c.x * d.x, c.y * d.y, c.z * d.z)), 2.0);
     double b = 0.0;
     b = b + bv.x;
@@ -502,7 +522,6 @@ __device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p
     double delta_squared = b * b - 4.0 * a * cc;
     if (delta_squared < 0.0) return -1.0;
     double delta = sqrt(delta_squared);
-    double one_over_2_a = 1.0 / (2.0 * a);
     double t1 = (-b - delta) * one_over_2_a;
     double t2 = (-b + delta) * one_over_2_a;
     double distance = (t1 < 0.0 || (t2 >= 0.0 && t1 >= t2)) ? t2 : t1;
@@ -769,7 +788,11 @@ __device__ __forceinline__ Best closest_hit(const DeviceScene& S, const RayPre& 
         double d;
         bool ok;
         if (pr.kind == 0) ok = plane_distance(pr, p, d);
-        else { d = sphere_distance(pr, p); ok = d >= 0.0; }
+        else {
+            const double a = sphere_a(p.d);
+            d = sphere_distance(pr, p, a, 1.0 / (2.0 * a));
+            ok = d >= 0.0;
+        }
         if (!ok) continue;
         bool take = !best.kind || d < best.d;  // NaN never replaces, never gets replaced
         if (take) {
@@ -794,7 +817,7 @@ __device__ bool any_hit(const DeviceScene& S, const RayPre& p, uint32_t* st, int
         double d;
         if (pr.kind == 0) {
             if (plane_distance(pr, p, d)) return true;
-        } else if (sphere_distance(pr, p) >= 0.0) {
+        } else if (sphere_distance(pr, p, sphere_a(p.d), 1.0 / (2.0 * sphere_a(p.d))) >= 0.0) {
             return true;
         }
     }

@@ -119,6 +119,12 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
+#ifndef VR_SPHERE_HOIST  // begin_ray: sphere a and 1 / (2a) once per ray (near-unit reciprocal)
+#define VR_SPHERE_HOIST 1
+#endif
+#ifndef VR_LEAF_SKIP  // node step: skip the FIFO append when no lane met a leaf
+#define VR_LEAF_SKIP 1
+#endif
 #ifndef VR_STAGE_NT  // staged photons written with the non-temporal hint (A/B: plain stores)
 #define VR_STAGE_NT 1
 #endif
@@ -450,6 +456,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         best.d = 0.0;
         best.index = -1;
         best.object = 0x7fffffff;
+#if VR_SPHERE_HOIST
+        double sa = 0.0, s2a = 0.0;  // the ray's sphere a and 1 / (2a), once per ray
+        bool have_a = false;
+#endif
         for (int i = 0; i < S.prim_count; ++i) {
             const Prim& pr = S.prims[i];
             double dd;
@@ -478,7 +488,19 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #else
                 if (__ballot(!sphere_missed32(pr, pre)) == 0) continue;
 #endif
-                dd = sphere_distance(pr, pre);
+#if VR_SPHERE_HOIST
+                if (!have_a) {  // wave-uniform: the first sphere this ray's wave tests exactly
+                    sa = sphere_a(pre.d);
+                    s2a = half_recip_near1(sa);
+                    have_a = true;
+                }
+                dd = sphere_distance(pr, pre, sa, s2a);
+#else
+                {
+                    const double a1 = sphere_a(pre.d);
+                    dd = sphere_distance(pr, pre, a1, 1.0 / (2.0 * a1));
+                }
+#endif
                 ok = dd >= 0.0;
             }
             if (ok && (!best.kind || dd < best.d)) {  // min_by keeps the first of equals
@@ -953,6 +975,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             __builtin_amdgcn_s_setprio(VR_PRIO_LEAF);
 #if VR_WAVE_LEAF
             // append this step's leaves to the wave FIFO in (child slot, lane) order
+#if VR_LEAF_SKIP
+            if (__ballot(lmask != 0u))
+#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool lh = (lmask >> k) & 1u;
