@@ -160,6 +160,13 @@ typedef struct vr_scene vr_scene;
  * identical either way (the closest hit does not depend on the tree; ties follow the reference
  * tree's in-order leaf rank); the device build always produces the reference tree. */
 #define VR_SCENE_REFERENCE_BVH 4u
+/* Build the default traversal tree on the device as well (ABI 5): the reference's median-split
+ * build above gives every triangle its in-order rank (the tie-break), then a binned-SAH binary
+ * tree (the host build's algorithm, one workgroup per node and level) is built over the ranked
+ * triangles and collapsed to the 4-wide render tree.  Renders are bit-identical to the host-built
+ * scene's; only the build time differs.  Implies VR_SCENE_DEVICE_BVH; ignored with
+ * VR_SCENE_REFERENCE_BVH or VR_SCENE_HOST_ONLY. */
+#define VR_SCENE_DEVICE_SAH 8u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split

@@ -112,3 +112,60 @@ def test_device_build_c5_mesh():
     print(f"C5 build: device {t_dev:.3f} s, host {t_host:.3f} s; wide nodes {dev.info()['wide_node_count']}, "
           f"stack {dev.info()['traversal_stack']}")
     _render_equal(s.device_scene(0), dev)
+
+
+# ---------------------------------------------------------------- the SAH traversal tree on the device
+def _sah_tree_is_valid(ds, n):
+    """The device SAH tree: n - 1 interior nodes, every triangle in exactly one leaf, every child
+    box containing its subtree's triangle boxes (the union rule the conservative walk relies on)."""
+    nodes = ds.bvh_nodes()
+    assert len(nodes) == n - 1
+    leaves = np.sort(~nodes["child"][nodes["child"] < 0])
+    assert np.array_equal(leaves, np.arange(n))
+    inner = nodes["child"][nodes["child"] >= 0]
+    assert len(np.unique(inner)) == len(inner) == n - 2  # every non-root interior node once
+    for i in range(len(nodes)):
+        for c in range(2):
+            ch = nodes["child"][i, c]
+            if ch >= 0:  # a child node's own boxes lie inside the box the parent keeps for it
+                pb = nodes["box"][i, c]
+                for cc in range(2):
+                    b = nodes["box"][ch, cc]
+                    assert (b[0::2] >= pb[0::2]).all() and (b[1::2] <= pb[1::2]).all()
+
+
+@pytest.mark.parametrize("n", [2, 3, 17, 1000, 4097])
+def test_device_sah_tree_renders_like_the_host_tree(n):
+    rng = np.random.default_rng(100 + n)
+    s = _mesh_scene(_random_mesh(rng, n, ties=n == 1000))
+    dev = s.device_scene(0, device_sah=True)
+    host = s.device_scene(0)
+    assert np.array_equal(dev.leaf_order(0), host.leaf_order(0))  # the reference ranks
+    _sah_tree_is_valid(dev, n)
+    _render_equal(host, dev)
+
+
+def test_device_sah_bunny_and_c5():
+    """The default traversal tree built on the device: the main.rs scene renders bit-identically
+    to the host-built scene, and the C5 mesh builds in well under a second."""
+    import torch
+    s = scenes.main_scene(scenes.procedural_bunny())
+    dev, host = s.device_scene(0, device_sah=True), s.device_scene(0)
+    assert dev.info()["traversal_stack"] <= 47 and dev.info()["nan_free"]
+    _render_equal(host, dev, W=160, H=120)
+    v, n = scenes.synthetic_sphere_mesh()
+    c5 = Scene(scenes.CAMERA_LOCATION, [BoundingVolumeHierarchy.build(Mesh(v, n, LambertianMaterial(
+        Spectrum.grey(0.5), 0.5)))])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d5 = c5.device_scene(0, device_sah=True)
+    t_dev = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    h5 = c5.device_scene(0)
+    t_host = time.perf_counter() - t0
+    i5 = d5.info()
+    print(f"C5 SAH build: device {t_dev:.3f} s, host {t_host:.3f} s; wide nodes {i5['wide_node_count']} "
+          f"(host {h5.info()['wide_node_count']}), stack {i5['traversal_stack']}, depth {i5['max_bvh_depth']}")
+    assert t_dev < 1.0
+    assert np.array_equal(d5.leaf_order(0), h5.leaf_order(0))
+    _render_equal(h5, d5, W=64, H=48)

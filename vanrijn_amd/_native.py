@@ -22,6 +22,7 @@ OBJECT_PRIMITIVE_LIST, OBJECT_BVH = 0, 1
 SCENE_HOST_ONLY = 1
 SCENE_DEVICE_BVH = 2
 SCENE_REFERENCE_BVH = 4
+SCENE_DEVICE_SAH = 8
 LAUNCH_TIMED, LAUNCH_COUNTERS = 1, 2
 SCENE_INFO_NAN_FREE = 1
 

@@ -205,6 +205,277 @@ __global__ void fill_wide_kernel(const Node* bin, const int32_t* desc, uint64_t 
     out4[i] = w;
 }
 
+// ------------------------------------------------------------------------------------------------
+// The default traversal tree on the device (VR_SCENE_DEVICE_SAH): the binned-SAH binary tree of
+// vr_host.cpp SahBuilder, built top-down one level at a time, one workgroup per segment of the
+// level.  Its input is the reference-order triangle array the median build above leaves (each
+// TriVerts carries its reference in-order rank, which breaks distance ties);
+// its output is the SAH binary tree and the triangles permuted into its leaf order.  The tree
+// differs from the host's only where the host's unstable std::partition / nth_element order equal
+// keys: renders are bit-identical for any tree, only the work differs.
+//
+// Per segment [lo, hi) of positions (pos -> reference index perm[pos]):
+//   1. the node box (union of the triangles' boxes) and the centroid bounds, reduced over the
+//      workgroup; the box goes into the parent's child slot (or the root box);
+//   2. 32 bins per axis over the centroid bounds: counts and bin boxes in LDS (64-bit atomics on
+//      order-preserving bits of the doubles);
+//   3. the split with the least area(left) * n_left + area(right) * n_right (axes and bins in
+//      order, the first minimum wins -- the host's loops); none, or the depth cap of the
+//      traversal stack reached (level + ceil(log2 n) >= 44, as the host): split at the middle;
+//   4. a stable partition of the segment's positions into perm_out, then the two child segments
+//      (node indices from an atomic counter; any numbering serves, the 4-wide collapse renumbers).
+// ------------------------------------------------------------------------------------------------
+struct SahSeg {
+    uint32_t lo, hi;
+    int32_t node;    // interior index (n >= 2) or -1
+    int32_t parent;  // parent's interior index, -1 for the root
+    int32_t which;   // child slot in the parent
+    int32_t level;
+};
+
+constexpr int kSahBins = 32;
+
+__device__ __forceinline__ uint64_t omin_bits(double x) { return order_bits(x); }
+__device__ __forceinline__ double from_order_bits(uint64_t b) {
+    const uint64_t r = (b >> 63) ? (b & 0x7FFFFFFFFFFFFFFFull) : ~b;
+    return __longlong_as_double((long long)r);
+}
+
+// reference-order triangles -> per-position box and centroid (BoundingBox::from_points, centre())
+__global__ void sah_prims_kernel(const TriVerts* tris, uint32_t n, BoxD* boxes, double* centres, uint32_t* perm) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const TriVerts tv = tris[t];
+    BoxD b;
+    for (int c = 0; c < 3; ++c) b.mn[c] = b.mx[c] = tv.v[c];
+    for (int k = 1; k < 3; ++k)
+        for (int c = 0; c < 3; ++c) {
+            b.mn[c] = fmin(b.mn[c], tv.v[3 * k + c]);
+            b.mx[c] = fmax(b.mx[c], tv.v[3 * k + c]);
+        }
+    boxes[t] = b;
+    for (int c = 0; c < 3; ++c) centres[3 * (uint64_t)t + c] = (b.mn[c] + b.mx[c]) / 2.0;
+    perm[t] = t;
+}
+
+__device__ __forceinline__ double sah_area(const double mn[3], const double mx[3]) {
+    const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+    if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+__global__ __launch_bounds__(256) void sah_level_kernel(const SahSeg* segs, uint32_t nseg, const BoxD* boxes,
+                                                        const double* centres, const uint32_t* perm_in,
+                                                        uint32_t* perm_out, uint32_t* leaf_perm, Node* nodes,
+                                                        int32_t node_base,
+                                                        int32_t tri_base, double* root_box, SahSeg* next,
+                                                        uint32_t* next_count, uint32_t* node_count,
+                                                        uint32_t* max_level) {
+    __shared__ double r_mn[4][6], r_mx[4][6];  // per wave: box min / max (0..2), centroid (3..5)
+    __shared__ uint32_t cnt[3][kSahBins];
+    __shared__ unsigned long long bmn[3][kSahBins][3], bmx[3][kSahBins][3];
+    __shared__ int s_axis, s_bin;
+    __shared__ double s_cmin[3], s_scale[3];
+    __shared__ uint32_t s_nl, s_base_l, s_base_r, s_wave_l[4];
+    const uint32_t si = blockIdx.x;
+    if (si >= nseg) return;
+    const SahSeg g = segs[si];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t n = g.hi - g.lo;
+    // 1. node box and centroid bounds
+    double mn[6], mx[6];
+    for (int c = 0; c < 6; ++c) {
+        mn[c] = INFINITY;
+        mx[c] = -INFINITY;
+    }
+    for (uint32_t p = g.lo + tid; p < g.hi; p += 256) {
+        const uint32_t r = perm_in[p];
+        const BoxD b = boxes[r];
+        for (int c = 0; c < 3; ++c) {
+            mn[c] = fmin(mn[c], b.mn[c]);
+            mx[c] = fmax(mx[c], b.mx[c]);
+            const double ce = centres[3 * (uint64_t)r + c];
+            mn[3 + c] = fmin(mn[3 + c], ce);
+            mx[3 + c] = fmax(mx[3 + c], ce);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1)
+        for (int c = 0; c < 6; ++c) {
+            mn[c] = fmin(mn[c], __shfl_xor(mn[c], off));
+            mx[c] = fmax(mx[c], __shfl_xor(mx[c], off));
+        }
+    if (lane == 0)
+        for (int c = 0; c < 6; ++c) {
+            r_mn[wv][c] = mn[c];
+            r_mx[wv][c] = mx[c];
+        }
+    for (uint32_t i = tid; i < 3 * kSahBins; i += 256) {
+        cnt[i / kSahBins][i % kSahBins] = 0;
+        for (int c = 0; c < 3; ++c) {
+            bmn[i / kSahBins][i % kSahBins][c] = ~0ull;
+            bmx[i / kSahBins][i % kSahBins][c] = 0ull;
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < 6; ++c) {
+        mn[c] = fmin(fmin(r_mn[0][c], r_mn[1][c]), fmin(r_mn[2][c], r_mn[3][c]));
+        mx[c] = fmax(fmax(r_mx[0][c], r_mx[1][c]), fmax(r_mx[2][c], r_mx[3][c]));
+    }
+    if (tid == 0) {
+        double box[6];
+        for (int c = 0; c < 3; ++c) {
+            box[2 * c] = mn[c];
+            box[2 * c + 1] = mx[c];
+        }
+        if (g.parent >= 0) {
+            Node& pn = nodes[g.parent];
+            for (int i = 0; i < 6; ++i) pn.box[g.which][i] = box[i];
+            pn.child[g.which] = n >= 2 ? node_base + g.node : ~(tri_base + (int32_t)g.lo);
+        } else {
+            for (int i = 0; i < 6; ++i) root_box[i] = box[i];
+        }
+        atomicMax(max_level, (uint32_t)g.level + 1);
+    }
+    if (n < 2) {  // a leaf: its triangle's final position is lo
+        if (tid == 0) leaf_perm[g.lo] = perm_in[g.lo];
+        return;
+    }
+    // 2. binning (axes with a positive centroid extent)
+    const int need = 32 - __clz((int)(n - 1));  // ceil(log2 n)
+    const bool sah = g.level + need < 44;
+    if (tid < 3) {
+        const double ext = mx[3 + tid] - mn[3 + tid];
+        s_cmin[tid] = mn[3 + tid];
+        s_scale[tid] = ext > 0.0 ? kSahBins / ext : 0.0;
+    }
+    __syncthreads();
+    if (sah) {
+        for (uint32_t p = g.lo + tid; p < g.hi; p += 256) {
+            const uint32_t r = perm_in[p];
+            const BoxD b = boxes[r];
+            for (int a = 0; a < 3; ++a) {
+                if (!(s_scale[a] > 0.0)) continue;
+                int k = (int)((centres[3 * (uint64_t)r + a] - s_cmin[a]) * s_scale[a]);
+                k = k < 0 ? 0 : (k > kSahBins - 1 ? kSahBins - 1 : k);
+                atomicAdd(&cnt[a][k], 1u);
+                for (int c = 0; c < 3; ++c) {
+                    atomicMin(&bmn[a][k][c], (unsigned long long)omin_bits(b.mn[c]));
+                    atomicMax(&bmx[a][k][c], (unsigned long long)omin_bits(b.mx[c]));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // 3. the cheapest split (thread 0: 3 axes x 31 candidate planes)
+    if (tid == 0) {
+        int best_axis = -1, best_bin = -1;
+        double best_cost = INFINITY;
+        uint32_t best_nl = 0;
+        for (int a = 0; sah && a < 3; ++a) {
+            if (!(s_scale[a] > 0.0)) continue;
+            double rarea[kSahBins];
+            uint32_t rcnt[kSahBins];
+            double amn[3] = {INFINITY, INFINITY, INFINITY}, amx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t c = 0;
+            for (int k = kSahBins - 1; k > 0; --k) {
+                if (cnt[a][k])
+                    for (int j = 0; j < 3; ++j) {
+                        amn[j] = fmin(amn[j], from_order_bits(bmn[a][k][j]));
+                        amx[j] = fmax(amx[j], from_order_bits(bmx[a][k][j]));
+                    }
+                c += cnt[a][k];
+                rarea[k] = sah_area(amn, amx);
+                rcnt[k] = c;
+            }
+            for (int j = 0; j < 3; ++j) {
+                amn[j] = INFINITY;
+                amx[j] = -INFINITY;
+            }
+            c = 0;
+            for (int k = 0; k < kSahBins - 1; ++k) {
+                if (cnt[a][k])
+                    for (int j = 0; j < 3; ++j) {
+                        amn[j] = fmin(amn[j], from_order_bits(bmn[a][k][j]));
+                        amx[j] = fmax(amx[j], from_order_bits(bmx[a][k][j]));
+                    }
+                c += cnt[a][k];
+                if (c == 0 || rcnt[k + 1] == 0) continue;
+                const double cost = sah_area(amn, amx) * (double)c + rarea[k + 1] * (double)rcnt[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_bin = k;
+                    best_nl = c;
+                }
+            }
+        }
+        s_axis = best_axis;
+        s_bin = best_bin;
+        s_nl = best_axis >= 0 ? best_nl : n / 2;  // no split found / depth cap: the middle
+        s_base_l = 0;
+        s_base_r = 0;
+    }
+    __syncthreads();
+    // 4. stable partition, 256 positions at a time
+    const int axis = s_axis, bin = s_bin;
+    const uint32_t nl = s_nl;
+    for (uint32_t t0 = g.lo; t0 < g.hi; t0 += 256) {
+        const uint32_t p = t0 + tid;
+        const bool in = p < g.hi;
+        uint32_t r = 0;
+        bool left = false;
+        if (in) {
+            r = perm_in[p];
+            if (axis >= 0) {
+                int k = (int)((centres[3 * (uint64_t)r + axis] - s_cmin[axis]) * s_scale[axis]);
+                k = k < 0 ? 0 : (k > kSahBins - 1 ? kSahBins - 1 : k);
+                left = k <= bin;
+            } else {
+                left = p - g.lo < nl;
+            }
+        }
+        const uint64_t ml = __ballot(in && left), mr = __ballot(in && !left);
+        if (lane == 0) s_wave_l[wv] = (uint32_t)__popcll(ml) | ((uint32_t)__popcll(mr) << 16);
+        __syncthreads();
+        uint32_t bl = s_base_l, br = s_base_r;
+        for (uint32_t w = 0; w < wv; ++w) {
+            bl += s_wave_l[w] & 0xffff;
+            br += s_wave_l[w] >> 16;
+        }
+        const uint64_t below = (1ull << lane) - 1;
+        if (in) {
+            if (left) perm_out[g.lo + bl + (uint32_t)__popcll(ml & below)] = r;
+            else perm_out[g.lo + nl + br + (uint32_t)__popcll(mr & below)] = r;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 0; w < 4; ++w) {
+                s_base_l += s_wave_l[w] & 0xffff;
+                s_base_r += s_wave_l[w] >> 16;
+            }
+        }
+        __syncthreads();
+    }
+    // the child segments of the next level
+    if (tid == 0) {
+        const uint32_t nr = n - nl;
+        const uint32_t slot = atomicAdd(next_count, 2u);
+        const int32_t ln = nl >= 2 ? (int32_t)atomicAdd(node_count, 1u) : -1;
+        const int32_t rn = nr >= 2 ? (int32_t)atomicAdd(node_count, 1u) : -1;
+        next[slot] = {g.lo, g.lo + nl, ln, g.node, 0, g.level + 1};
+        next[slot + 1] = {g.lo + nl, g.hi, rn, g.node, 1, g.level + 1};
+    }
+}
+
+// the triangles and normals into the tree's leaf order (ranks ride along in TriVerts)
+__global__ void sah_gather_kernel(const TriVerts* tin, const TriNormals* nin, const uint32_t* perm, uint32_t n,
+                                  TriVerts* tout, TriNormals* nout) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    tout[p] = tin[perm[p]];
+    nout[p] = nin[perm[p]];
+}
+
 }  // namespace build
 
 #define VRB(call)                                 \
@@ -332,6 +603,68 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
     VRB(hipMemcpyAsync(root_box, d_root.p, sizeof(double) * 6, hipMemcpyDeviceToHost, st));
     VRB(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < n; ++i) leaf_order[i] = p[i];
+    return 0;
+}
+
+// The SAH traversal tree of one mesh whose triangles (tris / normals, n of them, reference leaf
+// order with ranks) are already on the device: nodes[0 .. n-1) receive the binary tree (root at
+// 0, links node_base-relative made global), tris / normals are permuted into its leaf order.
+// root_box (host, 6 f64) and levels (host: depth) are returned.  Returns a hipError_t.
+int device_build_sah(TriVerts* tris, TriNormals* normals, uint32_t n, int32_t node_base, int32_t tri_base,
+                     Node* nodes, double* root_box, int* levels, void* stream) {
+    using namespace build;
+    hipStream_t st = (hipStream_t)stream;
+    if (n < 2) return 0;
+    DevBuf d_boxes, d_centres, d_perm, d_perm2, d_leaf, d_seg, d_seg2, d_ctr, d_root, d_tris, d_norms;
+    VRB(d_boxes.alloc(sizeof(BoxD) * (size_t)n));
+    VRB(d_centres.alloc(sizeof(double) * 3 * (size_t)n));
+    VRB(d_perm.alloc(sizeof(uint32_t) * (size_t)n));
+    VRB(d_perm2.alloc(sizeof(uint32_t) * (size_t)n));
+    VRB(d_leaf.alloc(sizeof(uint32_t) * (size_t)n));
+    VRB(hipMemsetAsync(nodes, 0, sizeof(Node) * (size_t)(n - 1), st));
+    VRB(d_seg.alloc(sizeof(SahSeg) * (size_t)n));
+    VRB(d_seg2.alloc(sizeof(SahSeg) * (size_t)n));
+    VRB(d_ctr.alloc(sizeof(uint32_t) * 4));  // next segment count, node count, max level
+    VRB(d_root.alloc(sizeof(double) * 6));
+    const dim3 blk(256);
+    auto grid = [](uint64_t m) { return dim3((unsigned)((m + 255) / 256)); };
+    hipLaunchKernelGGL(sah_prims_kernel, grid(n), blk, 0, st, (const TriVerts*)tris, n, (BoxD*)d_boxes.p,
+                       (double*)d_centres.p, (uint32_t*)d_perm.p);
+    VRB(hipGetLastError());
+    const SahSeg root = {0, n, 0, -1, 0, 0};
+    VRB(hipMemcpyAsync(d_seg.p, &root, sizeof root, hipMemcpyHostToDevice, st));
+    const uint32_t ctr0[4] = {0, 1, 0, 0};  // the root holds interior index 0
+    VRB(hipMemcpyAsync(d_ctr.p, ctr0, sizeof ctr0, hipMemcpyHostToDevice, st));
+    uint32_t* ctr = (uint32_t*)d_ctr.p;
+    SahSeg *cur = (SahSeg*)d_seg.p, *nxt = (SahSeg*)d_seg2.p;
+    uint32_t *pin = (uint32_t*)d_perm.p, *pout = (uint32_t*)d_perm2.p;
+    uint32_t nseg = 1;
+    while (nseg) {
+        VRB(hipMemsetAsync(ctr, 0, sizeof(uint32_t), st));
+        hipLaunchKernelGGL(sah_level_kernel, dim3(nseg), blk, 0, st, (const SahSeg*)cur, nseg,
+                           (const BoxD*)d_boxes.p, (const double*)d_centres.p, (const uint32_t*)pin, pout,
+                           (uint32_t*)d_leaf.p, nodes, node_base, tri_base, (double*)d_root.p, nxt, ctr, ctr + 1,
+                           ctr + 2);
+        VRB(hipGetLastError());
+        VRB(hipMemcpyAsync(&nseg, ctr, sizeof nseg, hipMemcpyDeviceToHost, st));
+        VRB(hipStreamSynchronize(st));
+        std::swap(cur, nxt);
+        std::swap(pin, pout);  // every position of an interior segment was partitioned into pout
+    }
+    uint32_t c[4];
+    VRB(hipMemcpyAsync(c, ctr, sizeof c, hipMemcpyDeviceToHost, st));
+    VRB(hipMemcpyAsync(root_box, d_root.p, sizeof(double) * 6, hipMemcpyDeviceToHost, st));
+    // triangles into leaf order (through copies: the gather reads the reference order)
+    VRB(d_tris.alloc(sizeof(TriVerts) * (size_t)n));
+    VRB(d_norms.alloc(sizeof(TriNormals) * (size_t)n));
+    VRB(hipMemcpyAsync(d_tris.p, tris, sizeof(TriVerts) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    VRB(hipMemcpyAsync(d_norms.p, normals, sizeof(TriNormals) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(sah_gather_kernel, grid(n), blk, 0, st, (const TriVerts*)d_tris.p,
+                       (const TriNormals*)d_norms.p, (const uint32_t*)d_leaf.p, n, tris, normals);
+    VRB(hipGetLastError());
+    VRB(hipStreamSynchronize(st));
+    if (c[1] != n - 1) return (int)hipErrorUnknown;  // every interior node allocated exactly once
+    *levels = (int)c[2];
     return 0;
 }
 

@@ -438,6 +438,7 @@ struct vr_scene {
     // VR_SCENE_DEVICE_BVH: the meshes' BVHs are built on the device after upload (host vectors
     // nodes / tris / normals stay empty; the counts below size the device arrays)
     bool device_bvh = false;
+    bool device_sah = false;  // VR_SCENE_DEVICE_SAH: the SAH traversal tree too (vr_build.hip)
     uint64_t node_count = 0, tri_count = 0;
     struct PendingMesh {
         const double* vertices;
@@ -727,6 +728,37 @@ int upload(vr_scene* s) {
             s->max_depth = std::max(s->max_depth, levels);
         }
         VR_HIP(hipStreamSynchronize(cs.stream));
+        if (s->device_sah && s->device_bvh) {
+            // the SAH traversal tree over the ranked triangles (replaces the median tree in the
+            // binary array; the triangles move into its leaf order), then the 4-wide collapse on
+            // the host's binary copy (WideBuilder: depth-first layout, as the host-built scene)
+            for (const auto& pm : s->pending) {
+                if (pm.n < 2) continue;
+                double root_box[6];
+                int levels = 0;
+                const int e = vr::device_build_sah((vr::TriVerts*)(base + off[1]) + pm.tri_base,
+                                                   (vr::TriNormals*)(base + off[2]) + pm.tri_base, (uint32_t)pm.n,
+                                                   pm.node_base, pm.tri_base, nodes + pm.node_base, root_box, &levels,
+                                                   cs.stream);
+                if (e) return fail(VR_ERROR_DEVICE, std::string("device SAH build failed: ") +
+                                                        hipGetErrorString((hipError_t)e));
+                s->max_depth = std::max(s->max_depth, levels);
+            }
+            s->nodes.resize(s->node_count);
+            if (s->node_count)
+                VR_HIP(hipMemcpy(s->nodes.data(), nodes, s->node_count * sizeof(vr::Node), hipMemcpyDeviceToHost));
+            collapse_wide(s, s->nodes);
+            s->nodes.clear();
+            s->nodes.shrink_to_fit();
+            s->pending.clear();
+            if (sz_bvh) VR_HIP(hipMemcpy(base + off[5], s->bvhs.data(), sz_bvh, hipMemcpyHostToDevice));
+            if (!s->nodes4.empty())
+                VR_HIP(hipMemcpy(base + off[7], s->nodes4.data(), s->nodes4.size() * sizeof(vr::Node4),
+                                 hipMemcpyHostToDevice));
+            s->nodes4.clear();
+            s->nodes4.shrink_to_fit();
+            return VR_OK;
+        }
         // the 4-wide traversal tree: planned from the meshes' sizes (ShapeWide), boxes gathered on
         // the device
         ShapeWide W;
@@ -1179,7 +1211,8 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     s->mesh_tri_base.assign(desc->mesh_count, 0);
     // device build: requested, a device exists for it, and no NaN coordinate (the reference's
     // sort comparator maps NaN to Equal, which only the host build reproduces)
-    s->device_bvh = (flags & VR_SCENE_DEVICE_BVH) != 0 && !s->host_only;
+    s->device_bvh = (flags & (VR_SCENE_DEVICE_BVH | VR_SCENE_DEVICE_SAH)) != 0 && !s->host_only;
+    s->device_sah = (flags & VR_SCENE_DEVICE_SAH) != 0 && (flags & VR_SCENE_REFERENCE_BVH) == 0;
     // traversal tree: SAH (default) or the reference's own median-split tree
     const bool sah = (flags & VR_SCENE_REFERENCE_BVH) == 0 && !s->device_bvh;
     for (uint32_t mi = 0; s->device_bvh && mi < desc->mesh_count; ++mi) {

@@ -217,6 +217,10 @@ int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_
 int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32_t node_base, int32_t tri_base,
                      Node* nodes, TriVerts* tris, TriNormals* normals, uint64_t* leaf_order, double* root_box,
                      int* levels, void* stream);
+// vr_build.hip: the binned-SAH traversal tree of one mesh whose reference-order triangles are on the
+// device (root at nodes[0]); the triangles are permuted into its leaf order
+int device_build_sah(TriVerts* tris, TriNormals* normals, uint32_t n, int32_t node_base, int32_t tri_base,
+                     Node* nodes, double* root_box, int* levels, void* stream);
 // vr_build.hip: Node4 / Node4x records from a device-built binary tree and a host-made descriptor
 int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);

@@ -119,8 +119,11 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
-#ifndef VR_SPHERE_HOIST  // begin_ray: sphere a and 1 / (2a) once per ray (near-unit reciprocal)
-#define VR_SPHERE_HOIST 1
+// begin_ray's sphere test: 1 -- a and 1 / (2a) once per ray (near-unit reciprocal), kept live across
+// the primitive loop: rejected (main +1.0 %, bench +1.6 %, C5 -1.3 %, profiles/r03/ab_hoist_skip.txt);
+// 2 -- per sphere, 1 / (2a) by the near-unit reciprocal instead of the division; 0 -- the division
+#ifndef VR_SPHERE_HOIST
+#define VR_SPHERE_HOIST 0
 #endif
 #ifndef VR_LEAF_SKIP  // node step: skip the FIFO append when no lane met a leaf
 #define VR_LEAF_SKIP 1
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         best.d = 0.0;
         best.index = -1;
         best.object = 0x7fffffff;
-#if VR_SPHERE_HOIST
+#if VR_SPHERE_HOIST == 1
         double sa = 0.0, s2a = 0.0;  // the ray's sphere a and 1 / (2a), once per ray
         bool have_a = false;
 #endif
@@ -488,7 +491,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #else
                 if (__ballot(!sphere_missed32(pr, pre)) == 0) continue;
 #endif
-#if VR_SPHERE_HOIST
+#if VR_SPHERE_HOIST == 2
+                {
+                    const double a1 = sphere_a(pre.d);
+                    dd = sphere_distance(pr, pre, a1, half_recip_near1(a1));
+                }
+#elif VR_SPHERE_HOIST
                 if (!have_a) {  // wave-uniform: the first sphere this ray's wave tests exactly
                     sa = sphere_a(pre.d);
                     s2a = half_recip_near1(sa);

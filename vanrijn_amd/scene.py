@@ -292,19 +292,22 @@ class Scene:
             self._spec = SceneSpec(self.camera_location, mats, meshes, objs, self.integrator)
         return self._spec
 
-    def device_scene(self, device=0, host_only=False, device_bvh=False, reference_bvh=False):
-        key = (device, host_only, device_bvh, reference_bvh)
+    def device_scene(self, device=0, host_only=False, device_bvh=False, reference_bvh=False, device_sah=False):
+        key = (device, host_only, device_bvh, reference_bvh, device_sah)
         if key not in self._device_scenes:
-            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh, reference_bvh)
+            self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh, reference_bvh,
+                                                   device_sah)
         return self._device_scenes[key]
 
 
 class DeviceScene:
     """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
 
-    def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False, reference_bvh=False):
+    def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False, reference_bvh=False,
+                 device_sah=False):
         """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH: the reference's tree);
-        reference_bvh: traverse the reference's median-split tree instead of the SAH tree."""
+        reference_bvh: traverse the reference's median-split tree instead of the SAH tree;
+        device_sah: build the SAH traversal tree on the GPU too (VR_SCENE_DEVICE_SAH)."""
         L = N.lib()
         self.spec = spec
         keep = []  # keep ctypes buffers alive during vr_scene_create
@@ -350,7 +353,7 @@ class DeviceScene:
                            mats, prim_arr, mesh_arr, obj_arr, C.pointer(ig) if ig is not None else None)
         h = C.c_void_p()
         flags = ((N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0) |
-                 (N.SCENE_REFERENCE_BVH if reference_bvh else 0))
+                 (N.SCENE_REFERENCE_BVH if reference_bvh else 0) | (N.SCENE_DEVICE_SAH if device_sah else 0))
         N.check(L.vr_scene_create(C.byref(desc), device, flags, C.byref(h)))
         self.handle = h
         self.device = device
