@@ -17,3 +17,13 @@ SCENES="main:256 bench:32 c5:16" ROUNDS=3 timeout -k 10 900 bash tools/ab.sh abx
     > $O/ab_near1.txt 2>&1; ok $? ab; tail -7 $O/ab_near1.txt
 timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider \
     > $O/gpu_tests.log 2>&1; rc=$?; tail -3 $O/gpu_tests.log; ok $rc gpu-tests
+for c in "bench 256 16" "main 1024 1"; do
+  timeout -k 10 300 python tools/longpath.py $c >> $O/longpath.jsonl 2>> $O/longpath.err; ok $? "longpath $c"
+done
+cat $O/longpath.jsonl
+for sc in bench:256:16 main:1024:1 main:1024:64; do
+  IFS=: read -r scene size spp <<< "$sc"
+  timeout -k 10 400 python tools/variants.py --scene $scene --size $size --spp $spp --reps 3 --variants 0 \
+      --thresholds 52 --env VR_LEAF_FEW=0,4,8,16,64 >> $O/sweep_leaf_few_tail.jsonl 2>> $O/variants.err; ok $? "sweep $sc"
+done
+cut -c 1-160 $O/sweep_leaf_few_tail.jsonl

@@ -164,6 +164,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run `python -m vanrijn_amd.build` (hipcc, gfx950) first")
+        # torch's HIP runtime first: the library's libamdhip64 dependency then resolves to the one
+        # already loaded (same soname), so the library and torch share one runtime.  Loaded the
+        # other way round, torch would find the system runtime in place of its own and see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             try:

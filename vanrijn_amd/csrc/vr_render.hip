@@ -1004,10 +1004,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const uint32_t queued = q_tail - q_head;
             if (queued != 0) {
                 const bool stalled = np > 0 && (node < 0 || !(VR_ROOM));
-                // few lanes still traversing (a launch's tail, a long path alone in its wave): test
-                // their leaves at once, so the hits found tighten the distance cull of the rest of
-                // the walk -- waiting for a full round would walk the whole tree unculled
-                const bool few = __popcll(__ballot(state == kTraversing)) <= (int)A.leaf_few;
+                // the launch's tail (the queue is exhausted: some lane of the wave is done) with few
+                // lanes still traversing (long paths alone in their wave): test their leaves at once,
+                // so the hits found tighten the distance cull of the rest of the walk -- waiting for
+                // a full round would walk the whole tree unculled
+                const bool few = __ballot(state == kDone) != 0 &&
+                                 __popcll(__ballot(state == kTraversing)) <= (int)A.leaf_few;
                 if (queued >= A.leaf_threshold || few || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
                     __ballot(state == kTraversing && node >= 0 && VR_ROOM) == 0) {
                     VR_SEC(0);
