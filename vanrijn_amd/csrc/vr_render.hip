@@ -121,7 +121,8 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #endif
 // begin_ray's sphere test: 1 -- a and 1 / (2a) once per ray (near-unit reciprocal), kept live across
 // the primitive loop: rejected (main +1.0 %, bench +1.6 %, C5 -1.3 %, profiles/r03/ab_hoist_skip.txt);
-// 2 -- per sphere, 1 / (2a) by the near-unit reciprocal instead of the division; 0 -- the division
+// 2 -- per sphere, 1 / (2a) by the near-unit reciprocal instead of the division: rejected too (main
+// +1.6 %, bench and C5 +-0.5 %, profiles/r03/ab_sphere_near1.txt); 0 -- the division (default)
 #ifndef VR_SPHERE_HOIST
 #define VR_SPHERE_HOIST 0
 #endif
