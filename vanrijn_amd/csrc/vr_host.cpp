@@ -866,6 +866,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = getenv("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
+    const char* co = getenv("VR_COOP");  // tuning hook (A/B): 0 turns the cooperative tail off
+    a.coop = co ? (uint32_t)(atoi(co) != 0) : 1u;
     const char* lf = getenv("VR_LEAF_FEW");  // tuning hook (0: off)
     a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook

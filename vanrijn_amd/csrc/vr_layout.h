@@ -143,6 +143,7 @@ struct RenderArgs {
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     uint32_t leaf_few;            // ... or at most this many lanes are still traversing
+    uint32_t coop;                // 1: a wave's last path walks its tree with all lanes (the launch's tail)
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
