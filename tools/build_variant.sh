@@ -6,10 +6,12 @@ cd "$(dirname "$0")/.."
 NAME=$1; shift
 OUT=$(mktemp -d)
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall"
+pids=()
 for s in vr_render.hip vr_image.hip vr_build.hip vr_host.cpp; do
   /opt/rocm/bin/hipcc $FLAGS "$@" -c vanrijn_amd/csrc/$s -o $OUT/${s%.*}.o &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait "$p"; done  # set -e: a failed compile stops the link
 mkdir -p ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUT/*.o -lz -o ab/lib$NAME.so
 rm -rf "$OUT"

@@ -913,8 +913,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // (the other lanes are done).  Culling and the order-independent leaf rounds keep the
             // closest hit and its tie rule: only the visiting order changes.
             bool coop = false;
-#if VR_COOP && VR_WAVE_LEAF
             int owner = 0;
+#if VR_COOP && VR_WAVE_LEAF
             if (A.coop) {
                 const uint64_t live = __ballot(state != kDone);
                 coop = __popcll(live) == 1 && __ballot(state == kDone) != 0;
