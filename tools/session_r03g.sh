@@ -8,7 +8,10 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r03g}
 mkdir -p $O
 ok() { local rc=$1; shift; echo "$* rc=$rc"; [ "$rc" -eq 0 ] || exit "$rc"; }
-timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider \
+VR_LIBRARY=abx/libwatch.so timeout -k 10 300 python -u -m pytest tests/test_gpu_build.py tests/test_gpu_parity.py -x -v -s \
+    --timeout 100 --timeout-method thread -p no:cacheprovider > $O/watch_tests.log 2>&1; rc=$?
+grep -m 20 "watchdog" $O/watch_tests.log; tail -3 $O/watch_tests.log; ok $rc watch-tests
+timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
     > $O/gpu_tests.log 2>&1; rc=$?; tail -5 $O/gpu_tests.log; ok $rc gpu-tests
 for c in "bench 256 16" "main 1024 1" "main 512 64"; do
   timeout -k 10 300 python tools/tail.py $c >> $O/tail.jsonl 2>> $O/tail.err; ok $? "tail $c"

@@ -132,6 +132,9 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_COOP  // the launch's tail: a wave's last path walks its tree with every lane (RenderArgs::coop)
 #define VR_COOP 1
 #endif
+#ifndef VR_WATCHDOG
+#define VR_WATCHDOG 0
+#endif
 #ifndef VR_STAGE_NT  // staged photons written with the non-temporal hint (A/B: plain stores)
 #define VR_STAGE_NT 1
 #endif
@@ -893,7 +896,19 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         }
         if (__ballot(state != kDone) == 0) break;
         // ---------------------------------------------------------------- phase B: traverse
+#if VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
+        uint32_t wd = 0;
+#endif
         do {
+#if VR_WATCHDOG
+            if (++wd > (1u << 20)) {
+                printf("vr watchdog: block %u lane %u state %d node %d sp %d np %d q %u..%u bvh %d\n", blockIdx.x,
+                       lane, (int)state, node, sp, (int)np, q_head, q_tail, bvh_i);
+                atomicOr(A.error_flag, 1);
+                state = kDone;
+                break;
+            }
+#endif
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             VR_STAMP(5);
             VR_MARK("phaseB_top");
@@ -918,7 +933,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (A.coop) {
                 const uint64_t live = __ballot(state != kDone);
                 coop = __popcll(live) == 1 && __ballot(state == kDone) != 0;
-                owner = (int)__builtin_ctzll(live | 1ull);
+                owner = live ? (int)__builtin_ctzll(live) : 0;
             }
             if (coop) {
                 const int o_sp = __builtin_amdgcn_readlane(sp, owner);
