@@ -866,7 +866,9 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = getenv("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
-    const char* co = getenv("VR_COOP");  // tuning hook (A/B): 0 turns the cooperative tail off
+    // tuning hook (A/B): 0 turns the cooperative tail off in a build compiled with -DVR_COOP=1
+    // (the default build compiles it out: rejected, vr_render.hip)
+    const char* co = getenv("VR_COOP");
     a.coop = co ? (uint32_t)(atoi(co) != 0) : 1u;
     const char* lf = getenv("VR_LEAF_FEW");  // tuning hook (0: off)
     a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;

@@ -129,8 +129,13 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_LEAF_SKIP  // node step: skip the FIFO append when no lane met a leaf
 #define VR_LEAF_SKIP 1
 #endif
-#ifndef VR_COOP  // the launch's tail: a wave's last path walks its tree with every lane (RenderArgs::coop)
-#define VR_COOP 1
+// the launch's tail: a wave's last path walks its tree with every lane (RenderArgs::coop).  Parity-
+// green and the lone path 1.9x faster (profiles/r03/longpath_coop.jsonl), but rejected: inside the
+// node step main +5 %, C5 +9 % (profiles/r03/ab_coop_in_node_step.txt); as a tail-only call main
+// +1.5 %, C5 +6.7 %, bench scene +2 %, while C1 gains only 2.5 % -- its long paths share waves, so
+// one live lane per wave is rare (profiles/r03/ab_coop.txt, small_frames_coop.jsonl)
+#ifndef VR_COOP
+#define VR_COOP 0
 #endif
 #ifndef VR_WATCHDOG
 #define VR_WATCHDOG 0
@@ -741,6 +746,109 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         state = kRayReady;
     };
 
+#if VR_COOP && VR_WAVE_LEAF
+    // The launch's tail: the queue is exhausted and one path is left in the wave (a long path --
+    // e.g. 128 mirror bounces in a crease of the reflective bench scene -- makes a small frame's
+    // time).  Its walk is spread over the wave's lanes (VR_COOP): each step takes the current node
+    // and up to 63 entries from the top of the owner's stack, one per lane, tests them against the
+    // owner's ray, pushes the hit interior children back and queues the hit leaves for the owner;
+    // the stack spans every lane's column of the wave (the other lanes are done).  Culling and the
+    // order-independent leaf rounds keep the closest hit and its tie rule:
+    // only the visiting order changes.  Called with the whole wave active, owner wave-uniform; the
+    // main loop's node step pays one scalar branch for it.
+    auto coop_step = [&](const int owner) {
+        uint32_t lmask = 0;
+        int32_t lent[4];
+        const int o_sp = __builtin_amdgcn_readlane(sp, owner);
+        const int o_node = __builtin_amdgcn_readlane(node, owner);
+        const bool o_trav = __builtin_amdgcn_readlane(state == kTraversing ? 1 : 0, owner) != 0;
+        const int have = o_trav ? (o_node >= 0 ? 1 : 0) + o_sp : 0;
+        constexpr int kCap = 64 * STACK;  // the big stack: every lane column of the wave
+        // entries taken this step: at most 64, and at most what keeps 150 entries of
+        // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a
+        // near-full stack needs at most 3 per level below)
+        int t = have < 64 ? have : 64;
+        const int room = (kCap - 150 - have) / 3;
+        if (t > room) t = room < 1 ? (have > 0 ? 1 : 0) : room;
+        if (t > 0 && VR_ROOM) {
+            VR_MARK("coop_step");
+            // virtual stack index v of the owner -> its LDS word: v < STACK is the owner's own
+            // column (the usual layout), then the next lanes' columns in turn
+            auto vaddr = [&](int v) { return (v % STACK) * 256 + (tid & ~63) + ((owner + v / STACK) & 63); };
+            const int first_stack = o_node >= 0 ? 1 : 0;  // lane 0 takes the current node
+            int my = -1;
+            if ((int)lane < t) my = ((int)lane < first_stack) ? o_node : (int)st_node[vaddr(o_sp - 1 - ((int)lane - first_stack))];
+            const int base = o_sp - (t - first_stack);  // stack entries left below the taken ones
+            Ray32 r;  // the owner's ray and cull bounds, wave-uniform
+            r.ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ox), owner));
+            r.oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oy), owner));
+            r.oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oz), owner));
+            r.ix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ix), owner));
+            r.iy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iy), owner));
+            r.iz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iz), owner));
+            r.nx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nx), owner));
+            r.ny = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ny), owner));
+            r.nz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nz), owner));
+            r.ek = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ek), owner));
+            const float cf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_far), owner));
+            const float cb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_behind), owner));
+            uint32_t im = 0;  // hit interior children
+            int c[4];
+            if (my >= 0) {
+                const Node4& nd = VR_NODES4[my];
+                if (COUNT) cnt.node_visits++;
+                uint32_t xm = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    c[k] = nd.child[k];
+                    float f, g;
+                    bool maybe, sure;
+                    slab32_flags(nd.box[k], r, f, g, maybe, sure);
+                    const bool lv = c[k] != kEmptyChild;
+                    if (COUNT && lv) cnt.box_tests++;
+                    const bool pass = lv && maybe && !(f > cf || g < cb);
+                    xm |= (pass && !sure) ? 1u << k : 0u;
+                    im |= (pass && c[k] >= 0) ? 1u << k : 0u;
+                    lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
+                    lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
+                }
+            }
+            // interior hits onto the owner's stack, in (child slot, lane) order
+            int pos = base;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool ih = (im >> k) & 1u;
+                const uint64_t m = __ballot(ih);
+                if (ih) st_node[vaddr(pos + (int)__popcll(m & ((1ull << lane) - 1)))] = (uint32_t)c[k];
+                pos += (int)__popcll(m);
+            }
+            // the owner's next node: the top of its stack
+            if ((int)lane == owner) {
+                sp = pos;
+                if (sp > 0) {
+                    --sp;
+                    node = (int)st_node[vaddr(sp)];
+                } else {
+                    node = -1;
+                }
+            }
+        }
+        // the hit leaves, queued for the owner in (child slot, lane) order
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool lh = (lmask >> k) & 1u;
+            const uint64_t m = __ballot(lh);
+            if (lh) {
+                const uint32_t pos = (q_tail + (uint32_t)__popcll(m & ((1ull << lane) - 1))) & (kWaveList - 1);
+                wl_tri[wbase + pos] = lent[k];
+                wl_own[wbase + pos] = (uint8_t)owner;
+            }
+            q_tail += (uint32_t)__popcll(m);
+            if ((int)lane == owner) np += (int)__popcll(m);
+        }
+        q_tail = __builtin_amdgcn_readfirstlane(q_tail);
+    };
+#endif
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
@@ -895,6 +1003,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (__ballot(state == kTraversed) == 0) break;
         }
         if (__ballot(state != kDone) == 0) break;
+        const bool tail = __ballot(state == kDone) != 0;  // wave-uniform, fixed through phase B
+        (void)tail;
         // ---------------------------------------------------------------- phase B: traverse
 #if VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
         uint32_t wd = 0;
@@ -917,100 +1027,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #if VR_WAVE_LEAF
             uint32_t lmask = 0;  // leaf children this lane queues in this step
             int32_t lent[4];
-            uint32_t lowner = lane;  // the lane whose ray they belong to (the owner, in a tail step)
 #endif
-            // The launch's tail: the queue is exhausted and one path is left in the wave (a long
-            // path -- e.g. 128 mirror bounces in a crease of the reflective bench scene -- makes a
-            // small frame's time).  Its walk is spread over the wave's lanes (VR_COOP): each step
-            // takes the current node and up to 63 entries from the top of the owner's stack, one per
-            // lane, tests them against the owner's ray, pushes the hit interior children back and
-            // queues the hit leaves for the owner; the stack spans every lane's column of the wave
-            // (the other lanes are done).  Culling and the order-independent leaf rounds keep the
-            // closest hit and its tie rule: only the visiting order changes.
             bool coop = false;
-            int owner = 0;
 #if VR_COOP && VR_WAVE_LEAF
-            if (A.coop) {
+            if (A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
                 const uint64_t live = __ballot(state != kDone);
-                coop = __popcll(live) == 1 && __ballot(state == kDone) != 0;
-                owner = live ? (int)__builtin_ctzll(live) : 0;
-            }
-            if (coop) {
-                const int o_sp = __builtin_amdgcn_readlane(sp, owner);
-                const int o_node = __builtin_amdgcn_readlane(node, owner);
-                const bool o_trav = __builtin_amdgcn_readlane(state == kTraversing ? 1 : 0, owner) != 0;
-                const int have = o_trav ? (o_node >= 0 ? 1 : 0) + o_sp : 0;
-                constexpr int kCap = 64 * STACK;  // the big stack: every lane column of the wave
-                // entries taken this step: at most 64, and at most what keeps 150 entries of
-                // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a
-                // near-full stack needs at most 3 per level below)
-                int t = have < 64 ? have : 64;
-                const int room = (kCap - 150 - have) / 3;
-                if (t > room) t = room < 1 ? (have > 0 ? 1 : 0) : room;
-                if (t > 0 && VR_ROOM) {
-                    VR_MARK("coop_step");
-                    // virtual stack index v of the owner -> its LDS word: v < STACK is the owner's own
-                    // column (the usual layout), then the next lanes' columns in turn
-                    auto vaddr = [&](int v) { return (v % STACK) * 256 + (tid & ~63) + ((owner + v / STACK) & 63); };
-                    const int first_stack = o_node >= 0 ? 1 : 0;  // lane 0 takes the current node
-                    int my = -1;
-                    if ((int)lane < t) my = ((int)lane < first_stack) ? o_node : (int)st_node[vaddr(o_sp - 1 - ((int)lane - first_stack))];
-                    const int base = o_sp - (t - first_stack);  // stack entries left below the taken ones
-                    Ray32 r;  // the owner's ray and cull bounds, wave-uniform
-                    r.ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ox), owner));
-                    r.oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oy), owner));
-                    r.oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oz), owner));
-                    r.ix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ix), owner));
-                    r.iy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iy), owner));
-                    r.iz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iz), owner));
-                    r.nx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nx), owner));
-                    r.ny = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ny), owner));
-                    r.nz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nz), owner));
-                    r.ek = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ek), owner));
-                    const float cf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_far), owner));
-                    const float cb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_behind), owner));
-                    uint32_t im = 0;  // hit interior children
-                    int c[4];
-                    if (my >= 0) {
-                        const Node4& nd = VR_NODES4[my];
-                        if (COUNT) cnt.node_visits++;
-                        uint32_t xm = 0;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            c[k] = nd.child[k];
-                            float f, g;
-                            bool maybe, sure;
-                            slab32_flags(nd.box[k], r, f, g, maybe, sure);
-                            const bool lv = c[k] != kEmptyChild;
-                            if (COUNT && lv) cnt.box_tests++;
-                            const bool pass = lv && maybe && !(f > cf || g < cb);
-                            xm |= (pass && !sure) ? 1u << k : 0u;
-                            im |= (pass && c[k] >= 0) ? 1u << k : 0u;
-                            lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
-                            lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
-                        }
-                        lowner = (uint32_t)owner;
-                    }
-                    // interior hits onto the owner's stack, in (child slot, lane) order
-                    int pos = base;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const bool ih = (im >> k) & 1u;
-                        const uint64_t m = __ballot(ih);
-                        if (ih) st_node[vaddr(pos + (int)__popcll(m & ((1ull << lane) - 1)))] = (uint32_t)c[k];
-                        pos += (int)__popcll(m);
-                    }
-                    // the owner's next node: the top of its stack
-                    if ((int)lane == owner) {
-                        sp = pos;
-                        if (sp > 0) {
-                            --sp;
-                            node = (int)st_node[vaddr(sp)];
-                        } else {
-                            node = -1;
-                        }
-                    }
-                }
+                coop = __popcll(live) == 1;
+                if (coop) coop_step((int)__builtin_ctzll(live));
             }
 #endif
             if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
@@ -1107,12 +1130,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 if (lh) {
                     const uint32_t pos = (q_tail + (uint32_t)__popcll(m & ((1ull << lane) - 1))) & (kWaveList - 1);
                     wl_tri[wbase + pos] = lent[k];
-                    wl_own[wbase + pos] = (uint8_t)lowner;
+                    wl_own[wbase + pos] = (uint8_t)lane;
                 }
                 q_tail += (uint32_t)__popcll(m);
-                // pending leaves count for their owner (a tail step: every queued leaf is the owner's)
-                if (!coop) np += lh ? 1 : 0;
-                else if ((int)lane == owner) np += (int)__popcll(m);
+                np += lh ? 1 : 0;
             }
             q_tail = __builtin_amdgcn_readfirstlane(q_tail);
             // leaf round: leaf_threshold (64) queued leaves -- every lane busy --, or enough lanes (or
@@ -1124,7 +1145,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 // lanes still traversing (long paths alone in their wave): test their leaves at once,
                 // so the hits found tighten the distance cull of the rest of the walk -- waiting for
                 // a full round would walk the whole tree unculled
-                const bool few = coop || (__ballot(state == kDone) != 0 &&
+                const bool few = coop || (tail &&
                                           __popcll(__ballot(state == kTraversing)) <= (int)A.leaf_few);
                 if (queued >= A.leaf_threshold || few || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
                     __ballot(state == kTraversing && node >= 0 && VR_ROOM) == 0) {
