@@ -645,6 +645,80 @@ namespace {
 int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }  // binary tree walks
 int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render kernel (+1: branchless pushes)
 
+// Hot prefix: the top of the largest BVH's 4-wide tree moves to nodes4[0 .. k), which the render
+// kernel copies into LDS once per workgroup and reads from there (every ray that enters the BVH
+// starts its chain of dependent node fetches at the root).  The k nodes are chosen greedily by
+// surface area from the root (a child's box lies inside its parent's, so the set is a connected
+// top of the tree, and visits are roughly proportional to area); the other nodes keep their
+// depth-first order.  Only indices change: the walk, and so every result, is the same.
+int hot_node_budget() {
+    static const int k = getenv("VR_HOT_NODES") ? std::max(0, atoi(getenv("VR_HOT_NODES"))) : vr::kHotNodesDefault;
+    return std::min(k, vr::kHotNodesMax);
+}
+
+int hot_prefix(std::vector<vr::Node4>& n4, std::vector<vr::Bvh>& bvhs, int k) {
+    if (k <= 0 || n4.empty()) return 0;
+    // the BVH with the most wide nodes (each subtree is a contiguous depth-first range)
+    int32_t root = -1;
+    size_t most = 0;
+    for (const auto& b : bvhs) {
+        if (b.root4 < 0) continue;
+        size_t cnt = 0;
+        std::vector<int32_t> st{b.root4};
+        while (!st.empty()) {
+            const int32_t x = st.back();
+            st.pop_back();
+            ++cnt;
+            for (int c = 0; c < 4; ++c)
+                if (n4[x].child[c] >= 0) st.push_back(n4[x].child[c]);
+        }
+        if (cnt > most) {
+            most = cnt;
+            root = b.root4;
+        }
+    }
+    if (root < 0) return 0;
+    auto area = [](const float* b) {
+        const double dx = (double)b[1] - b[0], dy = (double)b[3] - b[2], dz = (double)b[5] - b[4];
+        return (dx >= 0.0 && dy >= 0.0 && dz >= 0.0) ? dx * dy + dy * dz + dz * dx : 0.0;
+    };
+    std::vector<int32_t> hot{root};
+    std::vector<std::pair<double, int32_t>> frontier;  // (area, node) of hot nodes' interior children
+    auto expand = [&](int32_t x) {
+        for (int c = 0; c < 4; ++c)
+            if (n4[x].child[c] >= 0) frontier.push_back({area(n4[x].box[c]), n4[x].child[c]});
+    };
+    expand(root);
+    while ((int)hot.size() < k && !frontier.empty()) {
+        size_t bi = 0;  // largest area; ties: the earlier node (deterministic)
+        for (size_t i = 1; i < frontier.size(); ++i)
+            if (frontier[i].first > frontier[bi].first ||
+                (frontier[i].first == frontier[bi].first && frontier[i].second < frontier[bi].second))
+                bi = i;
+        const int32_t x = frontier[bi].second;
+        frontier.erase(frontier.begin() + (ptrdiff_t)bi);
+        hot.push_back(x);
+        expand(x);
+    }
+    const int32_t n = (int32_t)n4.size();
+    std::vector<int32_t> perm(n, -1);
+    for (int32_t i = 0; i < (int32_t)hot.size(); ++i) perm[hot[i]] = i;
+    int32_t next = (int32_t)hot.size();
+    for (int32_t i = 0; i < n; ++i)
+        if (perm[i] < 0) perm[i] = next++;
+    std::vector<vr::Node4> out(n);
+    for (int32_t i = 0; i < n; ++i) {
+        vr::Node4 w = n4[i];
+        for (int c = 0; c < 4; ++c)
+            if (w.child[c] >= 0) w.child[c] = perm[w.child[c]];
+        out[perm[i]] = w;
+    }
+    n4.swap(out);
+    for (auto& b : bvhs)
+        if (b.root4 >= 0) b.root4 = perm[b.root4];
+    return (int)hot.size();
+}
+
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     s->nodes4.clear();
@@ -652,6 +726,7 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     for (auto& b : s->bvhs) b.root4 = b.root >= 0 ? W.collapse(b.root, 0) : b.root;
     s->wide_stack = W.stack;
     s->wide_count = s->nodes4.size();
+    s->dev.hot_count = hot_prefix(s->nodes4, s->bvhs, hot_node_budget());
 }
 
 template <class T>

@@ -12,6 +12,14 @@ namespace vr {
 constexpr int kRecursionLimit = 128;       // camera.rs:69
 constexpr int kMaxSpectrumSamples = 64;
 constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
+// LDS copy of the top of the 4-wide tree (DeviceScene::hot_count nodes, at most kHotNodesMax:
+// 4 KB of the render kernel's LDS per workgroup at 32); VR_HOT_NODES at scene creation lowers the
+// count.  Measured and rejected: off unless built with -DVR_HOT_MAX=16 / 32
+#ifndef VR_HOT_MAX
+#define VR_HOT_MAX 0
+#endif
+constexpr int kHotNodesMax = VR_HOT_MAX;
+constexpr int kHotNodesDefault = VR_HOT_MAX;
 
 // One interior node of a binary BVH, child boxes stored in the parent so a visit tests both
 // children with one 128-B record.  box[c] = {min x, max x, min y, max y, min z, max z} of child c
@@ -125,6 +133,11 @@ struct DeviceScene {
     int32_t light_base;
     int32_t sky_row;       // materials[sky_row]: knots / inv_step of the RGB basis (the sky lookup)
     const double* light_dirs;
+    // nodes4[0 .. hot_count): the top of the largest BVH's 4-wide tree (its root and the children
+    // with the largest boxes, greedily), which the render kernel copies into LDS once per
+    // workgroup (vr_host.cpp hot_prefix); 0: none
+    int32_t hot_count;
+    int32_t pad_hot;
 };
 
 struct RenderArgs {

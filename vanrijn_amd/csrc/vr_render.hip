@@ -200,6 +200,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #endif
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
+#if VR_HOT_MAX
+    // the top of the largest BVH's 4-wide tree (nodes4[0 .. hot_count), vr_host.cpp hot_prefix),
+    // copied once per workgroup: every ray entering that BVH starts its chain of dependent node
+    // fetches there, and those steps read LDS instead of L1 / L2
+    __shared__ uint4 hot4[VR_HOT_MAX * 8];
+    const uint32_t hot_n = (uint32_t)min(A.scene.hot_count, VR_HOT_MAX);
+    for (uint32_t i = tid; i < hot_n * 8; i += 256) hot4[i] = reinterpret_cast<const uint4*>(A.scene.nodes4)[i];
+    __syncthreads();
+#endif
 #if VR_WAVE_LEAF
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
     lr_key[tid] = 0;
@@ -1038,7 +1047,27 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #endif
             if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
+#if VR_HOT_MAX
+                // the node's 112 B (boxes, links): from LDS for the hot top of the tree
+                union {
+                    uint4 q[7];
+                    struct {
+                        float box[4][6];
+                        int32_t child[4];
+                    } n;
+                } nu;
+                if ((uint32_t)node < hot_n) {
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) nu.q[j] = hot4[node * 8 + j];
+                } else {
+                    const uint4* gq = reinterpret_cast<const uint4*>(VR_NODES4 + node);
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) nu.q[j] = gq[j];
+                }
+                const auto& nd = nu.n;
+#else
                 const Node4& nd = VR_NODES4[node];
+#endif
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
