@@ -418,8 +418,12 @@ __device__ __forceinline__ void slab32_flags(const float* b, const Ray32& r, flo
     const float e = r.ek + 3e-7f * (fabsf(lo) + fabsf(hi));
     tlo = lo - e;
     thi = hi + e;
-    sure = hi - lo > 2.0f * e;
-    maybe = sure || !(lo - hi > 2.0f * e);
+    // slab32's two tests on one difference: lo - hi is exactly -(hi - lo) (round to nearest), so
+    // !(lo - hi > 2e) is !(hi - lo < -2e) -- also true for a NaN difference -- and it holds
+    // whenever `sure` does (e >= 0)
+    const float d = hi - lo, e2 = 2.0f * e;
+    sure = d > e2;
+    maybe = !(d < -e2);
 }
 
 // A triangle record in one batch of five dwordx4 loads.  Left to itself the scheduler issued the

@@ -1027,8 +1027,20 @@ void ctx_free_all(CallCtx* c) {
 // back with ctx_release; work it enqueued may still run (its `done` event orders the next user).
 int ctx_acquire(vr_scene* s, CallCtx** out) {
     {
+        // a free context whose last call's work has finished on the device (its `done` has
+        // completed) first: one taken while its work is still queued orders the new call after it
+        // (hipStreamWaitEvent), which would serialise an asynchronous caller's frames on two
+        // streams; with none idle, a second context is created rather than waiting (so frame k + 1
+        // renders while frame k's launch drains), beyond two the most recent one is reused
         std::lock_guard<std::mutex> g(s->ctx_mutex);
-        if (!s->ctx_free.empty()) {
+        for (size_t i = s->ctx_free.size(); i-- > 0;) {
+            if (hipEventQuery(s->ctx_free[i]->done) == hipSuccess) {
+                *out = s->ctx_free[i];
+                s->ctx_free.erase(s->ctx_free.begin() + (ptrdiff_t)i);
+                return VR_OK;
+            }
+        }
+        if (!s->ctx_free.empty() && s->ctx_all.size() >= 2) {
             *out = s->ctx_free.back();
             s->ctx_free.pop_back();
             return VR_OK;

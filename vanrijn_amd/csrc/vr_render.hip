@@ -58,6 +58,10 @@ __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}
 // least `shade_threshold` lanes have finished, then those lanes shade and rejoin (one-ray-per-
 // iteration lock-step measured 25 % traversal lane utilisation; this scheme 58 %).
 // ----------------------------------------------------------------------------------------------
+// set bits of the wave mask m in lanes below this one (two v_mbcnt, no lane-mask registers)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 // Items of one launch: the first spp - tail samples in chunks of `chunk`, then the last `tail`
 // samples one per item, so that a path that runs to the recursion limit near the end of the
 // launch holds one lane for one path, not for `chunk` of them.
@@ -828,7 +832,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             for (int k = 0; k < 4; ++k) {
                 const bool ih = (im >> k) & 1u;
                 const uint64_t m = __ballot(ih);
-                if (ih) st_node[vaddr(pos + (int)__popcll(m & ((1ull << lane) - 1)))] = (uint32_t)c[k];
+                if (ih) st_node[vaddr(pos + (int)lanes_below(m))] = (uint32_t)c[k];
                 pos += (int)__popcll(m);
             }
             // the owner's next node: the top of its stack
@@ -848,7 +852,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const bool lh = (lmask >> k) & 1u;
             const uint64_t m = __ballot(lh);
             if (lh) {
-                const uint32_t pos = (q_tail + (uint32_t)__popcll(m & ((1ull << lane) - 1))) & (kWaveList - 1);
+                const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
                 wl_tri[wbase + pos] = lent[k];
                 wl_own[wbase + pos] = (uint8_t)owner;
             }
@@ -928,7 +932,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 VR_SEC(7);
                 VR_MARK("refill");
                 const unsigned leader = (unsigned)__builtin_ctzll(m);
-                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                const uint32_t rank = (uint32_t)lanes_below(m);
                 unsigned long long base = 0;
                 bool take = need;
                 if (A.grab == 0) {
@@ -1157,7 +1161,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const bool lh = (lmask >> k) & 1u;
                 const uint64_t m = __ballot(lh);
                 if (lh) {
-                    const uint32_t pos = (q_tail + (uint32_t)__popcll(m & ((1ull << lane) - 1))) & (kWaveList - 1);
+                    const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
                     wl_tri[wbase + pos] = lent[k];
                     wl_own[wbase + pos] = (uint8_t)lane;
                 }
