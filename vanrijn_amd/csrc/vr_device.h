@@ -57,6 +57,12 @@ __device__ __forceinline__ V3 normalize(V3 a) {  // vec3.rs:103-110 (multiply by
 #ifndef VR_NEAR1
 #define VR_NEAR1 1
 #endif
+// every active lane's b (bits of a.a minus bits of 1.0) within +-4096: one unsigned 64-bit compare
+// into a lane mask (llvm.amdgcn.icmp; a ballot of the two signed tests is lowered to two compares,
+// a v_cndmask and a v_cmp)
+__device__ __forceinline__ bool near1_all(int64_t b) {
+    return __builtin_amdgcn_uicmpl((uint64_t)(b + 4096), 8192ull, 34 /* ugt */) == 0;
+}
 __device__ __forceinline__ V3 normalize_n1(V3 a) {
 #if VR_NEAR1
     const double x = dot(a, a);
@@ -65,7 +71,7 @@ __device__ __forceinline__ V3 normalize_n1(V3 a) {
     double inv;
     // wave-uniform: the whole wave takes the bit formula or the sqrt and division (a divergent
     // branch would be if-converted into both)
-    if (__builtin_amdgcn_ballot_w64(!(b >= -4096 && b <= 4096)) == 0) {
+    if (near1_all(b)) {
         const int64_t j = b >= 0 ? (b >> 1) : ((1 - b) >> 1);  // s = 1 + j u  or  1 - j u/2
         inv = __longlong_as_double(b >= 0 ? one - 2 * j : one + ((j + 1) >> 1));
     } else {
@@ -503,7 +509,7 @@ __device__ __forceinline__ double sphere_a(V3 d) {
 __device__ __forceinline__ double half_recip_near1(double a) {
     const int64_t one = 0x3FF0000000000000ll;
     const int64_t b = __double_as_longlong(a) - one;
-    if (__builtin_amdgcn_ballot_w64(!(b >= -4096 && b <= 4096)) == 0)
+    if (near1_all(b))
         return 0.5 * __longlong_as_double(b >= 0 ? one - 2 * b : one + ((1 - b) >> 1));
     return 1.0 / (2.0 * a);
 }
@@ -539,6 +545,20 @@ __device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p
 // the f64 evaluation errs by O(1e-16 (|o|^2 + |c|^2 + |oc|^2)) and this f32 estimate of
 // dist^2 - r^2 by < 2e-6 |oc|^2 (|d| = 1 +- 1e-16; conversions, products and sums each 6e-8
 // relative), so the margin 1e-4 |oc|^2 + 1e-12 (|o|^2 + |c|^2) covers both.  NaN: not missed.
+__device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p);
+// lanes (of the active ones) whose sphere_missed32 is false, as one v_cmp: !(lhs > rhs) is
+// "unordered or less-equal"
+__device__ __forceinline__ uint64_t sphere_maybe32_lanes(const Prim& s, const RayPre& p) {
+    const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
+    const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
+    const float t = ox * dx + oy * dy + oz * dz;
+    const float oc2 = ox * ox + oy * oy + oz * oz;
+    const float r = (float)s.scalar;
+    const float po = (float)p.o.x * (float)p.o.x + (float)p.o.y * (float)p.o.y + (float)p.o.z * (float)p.o.z;
+    const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
+                     (float)s.vec[2] * (float)s.vec[2];
+    return __builtin_amdgcn_fcmpf((oc2 - t * t) - r * r, 1e-4f * oc2 + 1e-12f * (po + pc), 13 /* ule */);
+}
 __device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p) {
     const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
     const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;

@@ -58,6 +58,15 @@ __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}
 // least `shade_threshold` lanes have finished, then those lanes shade and rejoin (one-ray-per-
 // iteration lock-step measured 25 % traversal lane utilisation; this scheme 58 %).
 // ----------------------------------------------------------------------------------------------
+// Lane masks straight from one v_cmp into a scalar register pair (llvm.amdgcn.icmp): __ballot of a
+// bool that already lives in a lane mask is lowered to v_cndmask + v_cmp (two extra VALU per vote,
+// on the phase-B loop's every iteration)
+__device__ __forceinline__ uint64_t lanes_ieq(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 32); }
+__device__ __forceinline__ uint64_t lanes_ine(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 33); }
+__device__ __forceinline__ uint64_t lanes_igt(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 38); }
+__device__ __forceinline__ uint64_t lanes_ige(int a, int b) { return __builtin_amdgcn_sicmp(a, b, 39); }
+__device__ __forceinline__ uint64_t lanes_uge(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 35); }
+__device__ __forceinline__ uint64_t exec_mask() { return __builtin_amdgcn_read_exec(); }
 // set bits of the wave mask m in lanes below this one (two v_mbcnt, no lane-mask registers)
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -366,7 +375,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             rank = (uint32_t)tv.rank;
             if (COUNT && e >= 0) cnt.tri_tests++;
         }
-        if (__ballot(mine && e < 0 && (COUNT || d >= 0.0))) {
+        // lanes with an entry (lane < n) whose box was too close to call (e < 0) and whose triangle
+        // hits (d >= 0), as compares into lane masks
+        const uint64_t flagged = __builtin_amdgcn_uicmp(lane, n, 36 /* ult */) & lanes_igt(0, e);
+        if (COUNT ? flagged : (flagged & __builtin_amdgcn_fcmp(d, 0.0, 3 /* oge */))) {
             op.d.x = __shfl(pre.d.x, (int)owner);
             op.d.y = __shfl(pre.d.y, (int)owner);
             op.d.z = __shfl(pre.d.z, (int)owner);
@@ -514,7 +526,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const float bd = best.kind ? (float)best.d : INFINITY;
                 if (__ballot(!sphere_skip32(pr, pre, bd)) == 0) continue;
 #else
-                if (__ballot(!sphere_missed32(pr, pre)) == 0) continue;
+                if (sphere_maybe32_lanes(pr, pre) == 0) continue;
 #endif
 #if VR_SPHERE_HOIST == 2
                 {
@@ -876,9 +888,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // A shades them with more lanes busy (misses are finished at once either way)
             bool shade_now = true, finish_now = true;
             if (A.shade_min | A.miss_min) {
-                const bool idle = __ballot(state == kTraversing) == 0;
-                const int nhit = __popcll(__ballot(state == kTraversed && best.kind != kNone));
-                const int nmiss = __popcll(__ballot(state == kTraversed && best.kind == kNone));
+                const bool idle = lanes_ieq(state, kTraversing) == 0;
+                const uint64_t done_trav = lanes_ieq(state, kTraversed);
+                const int nhit = __popcll(done_trav & lanes_ine((int)best.kind, (int)kNone));
+                const int nmiss = __popcll(done_trav & lanes_ieq((int)best.kind, (int)kNone));
                 shade_now = nhit >= (int)A.shade_min || idle;
                 finish_now = nmiss >= (int)A.miss_min || idle;
             }
@@ -927,7 +940,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // refill: lanes whose item is exhausted take the next items (one atomic per wave)
             while (true) {
                 const bool need = state == kNeedRay && s_idx >= s_end;
-                const uint64_t m = __ballot(need);
+                const uint64_t m = lanes_ieq(state, kNeedRay) & lanes_uge(s_idx, s_end);
                 if (m == 0) break;
                 VR_SEC(7);
                 VR_MARK("refill");
@@ -1013,10 +1026,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             VR_STAMP(2);
 
-            if (__ballot(state == kTraversed) == 0) break;
+            if (lanes_ieq(state, kTraversed) == 0) break;
         }
-        if (__ballot(state != kDone) == 0) break;
-        const bool tail = __ballot(state == kDone) != 0;  // wave-uniform, fixed through phase B
+        if (lanes_ine(state, kDone) == 0) break;
+        const bool tail = lanes_ieq(state, kDone) != 0;  // wave-uniform, fixed through phase B
         (void)tail;
         // ---------------------------------------------------------------- phase B: traverse
 #if VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
@@ -1154,12 +1167,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
 #if VR_WAVE_LEAF
             // append this step's leaves to the wave FIFO in (child slot, lane) order
 #if VR_LEAF_SKIP
-            if (__ballot(lmask != 0u))
+            if (lanes_ine((int)lmask, 0))
 #endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool lh = (lmask >> k) & 1u;
-                const uint64_t m = __ballot(lh);
+                const uint64_t m = lanes_ine((int)(lmask & (1u << k)), 0);
                 if (lh) {
                     const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
                     wl_tri[wbase + pos] = lent[k];
@@ -1173,15 +1186,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // all) are stalled on theirs
             const uint32_t queued = q_tail - q_head;
             if (queued != 0) {
-                const bool stalled = np > 0 && (node < 0 || !(VR_ROOM));
                 // the launch's tail (the queue is exhausted: some lane of the wave is done) with few
                 // lanes still traversing (long paths alone in their wave): test their leaves at once,
                 // so the hits found tighten the distance cull of the rest of the walk -- waiting for
                 // a full round would walk the whole tree unculled
-                const bool few = coop || (tail &&
-                                          __popcll(__ballot(state == kTraversing)) <= (int)A.leaf_few);
-                if (queued >= A.leaf_threshold || few || __popcll(__ballot(stalled)) >= (int)A.leaf_stall ||
-                    __ballot(state == kTraversing && node >= 0 && VR_ROOM) == 0) {
+                const uint64_t trav = lanes_ieq(state, kTraversing);
+                const bool room = VR_ROOM;  // wave-uniform
+                const uint64_t at_node = trav & lanes_ige(node, 0);
+                const uint64_t stalled_m = lanes_igt(np, 0) & (room ? ~lanes_ige(node, 0) : exec_mask());
+                const bool few = coop || (tail && __popcll(trav) <= (int)A.leaf_few);
+                if (queued >= A.leaf_threshold || few || __popcll(stalled_m) >= (int)A.leaf_stall ||
+                    !room || at_node == 0) {
                     VR_SEC(0);
                     VR_MARK("leaf_test");
                     leaf_round(queued < 64u ? queued : 64u);
@@ -1213,8 +1228,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 ++bvh_i;
                 if (!start_bvhs()) state = kTraversed;
             }
-        } while (__ballot(state == kTraversing) != 0 &&
-                 __popcll(__ballot(state == kTraversed)) < (int)A.shade_threshold);
+        } while (lanes_ieq(state, kTraversing) != 0 &&
+                 __popcll(lanes_ieq(state, kTraversed)) < (int)A.shade_threshold);
     }
 
     if (COUNT) {
@@ -1421,7 +1436,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
             v[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p));
             dark = dark && __double_as_longlong(v[j].x) == 0 && __double_as_longlong(v[j].y) == 0;
         }
-        if (__ballot(!dark) == 0) {
+        if (__builtin_amdgcn_uicmp((uint32_t)dark, 0u, 32 /* eq */) == 0) {
             // a missed camera ray's photon {+0, +0} (camera.rs:110-113): every lobe is positive at
             // 0 nm, so its colour is (+0, +0, +0) exactly -- the wave skips the 28 exp when all
             // its photons are such (rows of pixels that see no geometry)
