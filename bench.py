@@ -51,8 +51,8 @@ sys.path.insert(0, ROOT)
 
 from vanrijn_amd import distributed as D  # noqa: E402
 from vanrijn_amd import scenes  # noqa: E402
-from vanrijn_amd.render import (AccumulationBuffer, Tile, partial_render_scene, render_tile_device,  # noqa: E402
-                                stream_check_error)
+from vanrijn_amd.render import (AccumulationBuffer, Tile, collect_launch_times, partial_render_scene,  # noqa: E402
+                                render_tile_device, stream_check_error)
 
 METRIC = "Msamples/s + achieved HBM GB/s, 1024x1024 bunny @256spp, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -479,11 +479,14 @@ def main():
 
     reduce_events = []
 
-    def step(i, timed=False):
+    def step(i, timed=False, defer=False):
+        # defer: the render's HIP events are recorded but not waited for (VR_LAUNCH_DEFER_TIMES), so
+        # back-to-back timed frames queue without a host round trip between them; their times are
+        # collected after the timed region
         def shard(first, st):
             return render_tile_device(dscene, tile, H, W, spp, SEED, first, st.data_ptr(), stream.cuda_stream,
-                                      timed=timed, device=local)
-        return D.frame_step(shard, state, i, spp, timer=reduce_events if timed else None)
+                                      timed=timed and not defer, defer_times=defer, device=local)
+        return D.frame_step(shard, state, i, spp, timer=reduce_events if timed or defer else None)
 
     if args.pmc_child:  # under rocprofv3 (live_pmc): one timed frame of the workload, nothing else
         step(1, timed=True)
@@ -498,19 +501,22 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, reduce_ms, passes = [], [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
-        st = step(1 + args.warmup + i, timed=True)
-        kernel_ms.append(st["kernel_ms"])  # render kernel only (HIP events on the launch stream)
-        reduce_ms.append(st["reduce_ms"])  # the ordered per-pixel Kahan reduce after it
-        passes.append(int(st.get("passes", 1)) or 1)  # launches per frame (staging cap)
+        step(1 + args.warmup + i, defer=True)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     stream_check_error(dscene, stream.cuda_stream, device=local)  # device errors of the untimed steps
+    # the timed frames' HIP-event times (render kernel on the launch stream; the ordered per-pixel
+    # Kahan reduce after it), and their device errors
+    lt = collect_launch_times(dscene, stream.cuda_stream, device=local)
+    assert lt["launches"] == args.steps, lt
+    kernel_ms = [lt["kernel_ms"] / args.steps]
+    reduce_ms = [lt["reduce_ms"] / args.steps]
+    passes = [max(1, lt["max_passes"])]  # launches per frame (staging cap)
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 5
+#define VR_ABI_VERSION 6
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -264,6 +264,10 @@ typedef struct vr_launch_stats {
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */
 #define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
+/* with VR_LAUNCH_TIMED: record the HIP events but return without waiting (stats: passes only); the
+ * times are read later by vr_collect_launch_times, so back-to-back timed frames leave the GPU no
+ * idle gap for a host round trip (ABI 6) */
+#define VR_LAUNCH_DEFER_TIMES 4u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
@@ -271,6 +275,18 @@ int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params,
  * vr_render_tile_device launch of `scene` on that stream since the last check, then clears it
  * (ABI 4).  A VR_LAUNCH_TIMED launch performs this check itself. */
 int vr_stream_check_error(const vr_scene* scene, void* stream);
+/* Waits for the VR_LAUNCH_DEFER_TIMES launches of `scene` on `stream` since the last collection
+ * and returns their summed HIP-event times, then forgets them; reports their device errors like
+ * vr_stream_check_error (ABI 6). */
+typedef struct vr_launch_times {
+    double kernel_ms;    /* render kernel, summed over the launches' passes */
+    double reduce_ms;    /* ordered per-pixel Kahan reduce, summed */
+    uint32_t launches;   /* vr_render_tile_device calls collected */
+    uint32_t passes;     /* render + reduce launches in them */
+    uint32_t max_passes; /* the most passes of one call */
+    uint32_t reserved;
+} vr_launch_times;
+int vr_collect_launch_times(const vr_scene* scene, void* stream, vr_launch_times* out);
 /* Mean XYZ of host-side state records: colour = colour_sum * (1 / weight)
  * (accumulation_buffer.rs:59).  States of disjoint sample sets (e.g. one per GPU) merge by
  * element-wise addition of the 8-double records (the cross-GPU reduce), which is what

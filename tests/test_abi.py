@@ -36,11 +36,12 @@ def test_struct_sizes_match_header():
     assert C.sizeof(N.RenderParams) == 72
     assert C.sizeof(N.SampleRecord) == 48
     assert C.sizeof(N.HitRecord) == 144
+    assert C.sizeof(N.LaunchTimes) == 32
 
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 5
+    assert lib.vr_abi_version() == 6
     assert isinstance(lib.vr_last_error(), bytes)
 
 

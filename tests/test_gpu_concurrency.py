@@ -18,7 +18,8 @@ import pytest
 
 from vanrijn_amd import _native as N
 from vanrijn_amd import scenes
-from vanrijn_amd.render import (Tile, partial_render_scene, render_tile, render_tile_device, stream_check_error)
+from vanrijn_amd.render import (Tile, collect_launch_times, partial_render_scene, render_tile, render_tile_device,
+                                stream_check_error)
 
 pytestmark = pytest.mark.gpu
 
@@ -137,3 +138,37 @@ def test_clean_scene_streams_check_ok(small_main):
     render_tile_device(ds, Tile(0, 32, 0, 32), 32, 32, 2, 3, 0, st.data_ptr(), s.cuda_stream)
     stream_check_error(ds, s.cuda_stream)
     assert float(st.reshape(-1, 8)[:, 6].sum()) == 2 * 32 * 32
+
+
+def test_deferred_launch_times(small_main, faulty_scene, monkeypatch):
+    """VR_LAUNCH_DEFER_TIMES (bench.py's timed frames): the launches queue without a host wait and
+    vr_collect_launch_times returns their summed event times once; the records equal timed launches'
+    bit for bit; device errors of deferred launches are reported by the collection."""
+    import torch
+    ds = small_main.device_scene(0)
+    s = torch.cuda.Stream()
+    t = Tile(0, 64, 0, 64)
+    a = torch.zeros(64 * 64 * 8, dtype=torch.float64, device="cuda")
+    b = torch.zeros_like(a)
+    assert collect_launch_times(ds, s.cuda_stream)["launches"] == 0  # nothing deferred yet
+    timed = [render_tile_device(ds, t, 64, 64, 4, 9, 4 * k, a.data_ptr(), s.cuda_stream, accumulate=k > 0,
+                                timed=True) for k in range(3)]
+    monkeypatch.setenv("VR_STAGING_CAP_MB", "1")  # 64^2 x 4 spp x 16 B = 256 KB: still one pass
+    for k in range(3):
+        st = render_tile_device(ds, t, 64, 64, 4, 9, 4 * k, b.data_ptr(), s.cuda_stream, accumulate=k > 0,
+                                defer_times=True)
+        assert st["timed"] == 0 and st["passes"] == 1
+    lt = collect_launch_times(ds, s.cuda_stream)
+    assert lt["launches"] == 3 and lt["passes"] == 3 and lt["max_passes"] == 1
+    assert lt["kernel_ms"] > 0 and lt["reduce_ms"] > 0
+    assert all(x["timed"] == 1 and x["kernel_ms"] > 0 for x in timed)
+    assert torch.equal(a, b)
+    assert collect_launch_times(ds, s.cuda_stream)["launches"] == 0  # collected once
+    # a deferred launch's singular basis is reported by the collection, then the stream is clean
+    fds, H, W, _ = faulty_scene
+    st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
+    render_tile_device(fds, Tile(0, W, 0, H), H, W, 1, 3, 0, st.data_ptr(), s.cuda_stream, defer_times=True)
+    with pytest.raises(N.VrError) as e:
+        collect_launch_times(fds, s.cuda_stream)
+    assert e.value.code == -5
+    stream_check_error(fds, s.cuda_stream)

@@ -29,4 +29,16 @@ out = {"scene": which, "spp": spp, "kernel_ms": st["kernel_ms"],
        "wave_executions": {k: int(v) for k, v in zip(["leaf_test", "leaf_test_2nd", "exact_box", "shade", "camera",
                                                         "begin_ray", "finish", "refill", "start_bvhs_trav"],
                                                        c[15:24])}, "counters": {k: st[k] for k in st if k not in ("kernel_ms", "timed")}}
+if len(c) >= 33:
+    # phase-B iterations by how many lanes take a node step in them (0, 1-8, .., 57-64): the
+    # headroom of merging waves' traversing lanes is the iterations a perfect
+    # packing of the same node steps would not need
+    h = c[24:33].astype(np.int64)
+    labels = ["0"] + ["%d-%d" % (8 * i + 1, 8 * i + 8) for i in range(8)]
+    out["node_step_lanes_hist"] = {k: int(v) for k, v in zip(labels, h)}
+    steps = int(h[1:].sum())
+    packed = int(np.ceil(st["node_visits"] / 64.0))
+    out["node_step_iterations"] = steps
+    out["node_step_iterations_perfectly_packed"] = packed
+    out["node_step_lane_utilisation"] = round(st["node_visits"] / (64.0 * max(1, steps)), 4)
 print(json.dumps(out))

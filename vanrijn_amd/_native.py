@@ -23,7 +23,7 @@ SCENE_HOST_ONLY = 1
 SCENE_DEVICE_BVH = 2
 SCENE_REFERENCE_BVH = 4
 SCENE_DEVICE_SAH = 8
-LAUNCH_TIMED, LAUNCH_COUNTERS = 1, 2
+LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES = 1, 2, 4
 SCENE_INFO_NAN_FREE = 1
 
 
@@ -113,6 +113,14 @@ class LaunchStats(C.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class LaunchTimes(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("reduce_ms", C.c_double), ("launches", C.c_uint32),
+                ("passes", C.c_uint32), ("max_passes", C.c_uint32), ("reserved", C.c_uint32)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
+
+
 class SampleRecord(C.Structure):
     _fields_ = [("wavelength", C.c_double), ("intensity", C.c_double), ("xyz", C.c_double * 3),
                 ("bounces", C.c_int32), ("flags", C.c_int32)]
@@ -136,6 +144,7 @@ SIGNATURES = {
     "vr_render_tile": (C.c_int, [_p, C.POINTER(RenderParams), C.POINTER(AccumulationBufferC)]),
     "vr_render_tile_device": (C.c_int, [_p, C.POINTER(RenderParams), _p, _p, _u32, C.POINTER(LaunchStats)]),
     "vr_stream_check_error": (C.c_int, [_p, _p]),
+    "vr_collect_launch_times": (C.c_int, [_p, _p, C.POINTER(LaunchTimes)]),
     "vr_resolve_state": (C.c_int, [_p, _u64, _p]),
     "vr_merge_tile": (C.c_int, [C.POINTER(AccumulationBufferC), TileC, C.POINTER(AccumulationBufferC)]),
     "vr_render_samples": (C.c_int, [_p, C.POINTER(RenderParams), _p]),

@@ -471,6 +471,14 @@ struct vr_scene {
     // read and cleared by vr_stream_check_error or a timed launch on that stream
     std::mutex slot_mutex;
     std::unordered_map<void*, int32_t*> stream_slots;
+    // deferred launch timings (VR_LAUNCH_DEFER_TIMES), per stream, under slot_mutex: the HIP events
+    // of launches not yet read by vr_collect_launch_times -- [start, mid, end] per pass -- and the
+    // passes of each launch
+    struct Deferred {
+        std::vector<hipEvent_t> ev;
+        std::vector<uint32_t> passes;
+    };
+    std::unordered_map<void*, Deferred> deferred;
     int cu_count = 0;
     uint64_t partial_seed = 0x5EED0001ull;
     // test hook (vr_debug_set_fault_object): hits on this object take the singular-basis path,
@@ -1459,6 +1467,8 @@ void vr_scene_destroy(vr_scene* s) {
         for (auto& kv : s->stream_slots) (void)hipFree(kv.second);
         if (s->d_block) (void)hipFree(s->d_block);
     }
+    for (auto& kv : s->deferred)
+        for (hipEvent_t e : kv.second.ev) (void)hipEventDestroy(e);
     delete s;
 }
 
@@ -1643,6 +1653,8 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     vr_scene* ms = const_cast<vr_scene*>(s);
     const bool counting = (launch_flags & VR_LAUNCH_COUNTERS) != 0;
     const bool timed = (launch_flags & VR_LAUNCH_TIMED) != 0 || counting;
+    // timed without waiting: the events stay with the scene until vr_collect_launch_times
+    const bool defer = timed && !counting && (launch_flags & VR_LAUNCH_DEFER_TIMES) != 0;
     int32_t* slot = nullptr;
     rc = stream_slot(ms, stream, &slot);
     if (rc) return rc;
@@ -1668,6 +1680,18 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         if (rc) return rc;
     }
     if (!timed) return VR_OK;  // errors of this launch: vr_stream_check_error(scene, stream)
+    if (defer) {
+        std::lock_guard<std::mutex> g(ms->slot_mutex);
+        vr_scene::Deferred& d = ms->deferred[stream];
+        d.ev.insert(d.ev.end(), pe.ev.begin(), pe.ev.end());
+        d.passes.push_back((uint32_t)(pe.ev.size() / 3));
+        pe.ev.clear();  // owned by the scene now
+        if (stats) {
+            std::memset(stats, 0, sizeof *stats);
+            stats->passes = d.passes.back();
+        }
+        return VR_OK;
+    }
     float render_ms = 0.f, reduce_ms = 0.f;
     if (!pe.ev.empty()) VR_HIP(hipEventSynchronize(pe.ev.back()));
     for (size_t i = 0; i + 3 <= pe.ev.size(); i += 3) {
@@ -1714,6 +1738,43 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         }
     }
     return read_and_clear_error(slot, st);
+}
+
+int vr_collect_launch_times(const vr_scene* s, void* stream, vr_launch_times* out) {
+    if (!s || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
+    VR_HIP(hipSetDevice(s->device));
+    vr_scene* ms = const_cast<vr_scene*>(s);
+    vr_scene::Deferred d;
+    int32_t* slot = nullptr;
+    {
+        std::lock_guard<std::mutex> g(ms->slot_mutex);
+        auto it = ms->deferred.find(stream);
+        if (it != ms->deferred.end()) {
+            d = std::move(it->second);
+            ms->deferred.erase(it);
+        }
+        auto sl = ms->stream_slots.find(stream);
+        if (sl != ms->stream_slots.end()) slot = sl->second;
+    }
+    PassEvents pe;  // destroys the events on every exit
+    pe.ev = std::move(d.ev);
+    std::memset(out, 0, sizeof *out);
+    if (!pe.ev.empty()) VR_HIP(hipEventSynchronize(pe.ev.back()));
+    for (size_t i = 0; i + 3 <= pe.ev.size(); i += 3) {
+        float x = 0.f, y = 0.f;
+        VR_HIP(hipEventElapsedTime(&x, pe.ev[i], pe.ev[i + 1]));
+        VR_HIP(hipEventElapsedTime(&y, pe.ev[i + 1], pe.ev[i + 2]));
+        out->kernel_ms += x;
+        out->reduce_ms += y;
+    }
+    out->launches = (uint32_t)d.passes.size();
+    for (uint32_t n : d.passes) {
+        out->passes += n;
+        out->max_passes = std::max(out->max_passes, n);
+    }
+    // the device errors of those launches, as a timed launch reports its own
+    return slot ? read_and_clear_error(slot, (hipStream_t)stream) : VR_OK;
 }
 
 int vr_stream_check_error(const vr_scene* s, void* stream) {

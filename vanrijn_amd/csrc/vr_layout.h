@@ -211,7 +211,9 @@ enum Counter : int {
     kCntSections = 15,       // 15..23: wave-level executions of code sections (diagnostic):
                              // leaf test, 2nd leaf test, exact box, shade, camera, begin_ray,
                              // finish, refill, start_bvhs in traversal
-    kCntCount = 24
+    kCntStepHist = 24,       // 24..32: phase-B iterations by the number n of lanes taking a node
+                             // step in them: n = 0, then 1-8, 9-16, .., 57-64 (diagnostic, VR_COUNTERS_PATH)
+    kCntCount = 33
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).

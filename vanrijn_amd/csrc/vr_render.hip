@@ -233,6 +233,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     S.bvhs = g_bvhs;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t sec[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t step_hist[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // counting variant: lanes per node step
 #ifdef VR_MARKS  // ISA section markers for tools/isa_sections.py (analysis builds only)
 #define VR_MARK(name) asm volatile(";@mark " name)
 #else
@@ -1055,6 +1056,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             int32_t lent[4];
 #endif
             bool coop = false;
+            if (COUNT) {  // how full this iteration's node step is (the headroom of merging waves)
+                const int n = VR_ROOM ? __popcll(lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) : 0;
+                if (first_active_lane()) step_hist[n == 0 ? 0 : 1 + (n - 1) / 8]++;
+            }
 #if VR_COOP && VR_WAVE_LEAF
             if (A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
                 const uint64_t live = __ballot(state != kDone);
@@ -1245,8 +1250,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         VR_STAMP(5);
         if (first_active_lane())
             for (int i = 0; i < 6; ++i) atomicAdd(&A.counters[kCntCycles + i], (unsigned long long)cyc[i]);
-        for (int i = 0; i < 9; ++i)  // each lane counted the executions it led
+        for (int i = 0; i < 9; ++i) {  // each lane counted the executions it led
             if (sec[i]) atomicAdd(&A.counters[kCntSections + i], (unsigned long long)sec[i]);
+            if (step_hist[i]) atomicAdd(&A.counters[kCntStepHist + i], (unsigned long long)step_hist[i]);
+        }
         if (A.wg_times) {
             __syncthreads();
             if (tid == 0) A.wg_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1421,7 +1428,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     if (mask) {
         const uint64_t py = p / tile_width, px = p - py * tile_width;
         if (mask[(py >> 3) * ((tile_width + 7) >> 3) + (px >> 3)]) {
-            // a culled block (block_cull_kernel): every sample is the photon {0, 0}, colour +0
+            // a culled block (block_cull_kernel): every sample is the photon {0, 0}, colour +0.
+            // From a fresh record the Kahan chain has a closed form: colour y = +0 * 1 - +0 = +0
+            // keeps sums and compensations +0, and the weight counts 1, 2, .., spp exactly with
+            // compensation (n + 1 - n) - 1 = 0 (spp < 2^32 < 2^53)
+            if (!accumulate) {
+                w = (double)spp;
+                s = spp;
+            }
             const double z[3] = {0.0, 0.0, 0.0};
             for (; s < spp; ++s) update(z);
         }

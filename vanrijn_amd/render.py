@@ -231,16 +231,28 @@ def trace_rays(scene, origins, directions, device=0):
 
 
 def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample, state_ptr, stream_ptr=None,
-                       accumulate=False, timed=False, counters=False, device=0):
+                       accumulate=False, timed=False, counters=False, device=0, defer_times=False):
     """Enqueue a render into device state records (8 f64 per pixel) at `state_ptr` (a device
-    pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel time when timed)."""
+    pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel time when timed;
+    `defer_times`: the events are recorded without waiting, read by collect_launch_times)."""
     ds = _scene_handle(scene, device)
     p = _params(tile, height, width, spp, seed, first_sample, accumulate)
     st = N.LaunchStats()
-    flags = (N.LAUNCH_TIMED if timed else 0) | (N.LAUNCH_COUNTERS if counters else 0)
+    flags = (N.LAUNCH_TIMED if timed or defer_times else 0) | (N.LAUNCH_COUNTERS if counters else 0) | \
+        (N.LAUNCH_DEFER_TIMES if defer_times else 0)
     N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
                                           C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
     return st.as_dict()
+
+
+def collect_launch_times(scene, stream_ptr=None, device=0):
+    """Waits for the defer_times launches of `scene` on the stream since the last collection:
+    {kernel_ms, reduce_ms (sums), launches, passes, max_passes} (vr_collect_launch_times); raises
+    their device errors like stream_check_error."""
+    ds = _scene_handle(scene, device)
+    t = N.LaunchTimes()
+    N.check(N.lib().vr_collect_launch_times(ds.handle, C.c_void_p(stream_ptr or 0), C.byref(t)))
+    return t.as_dict()
 
 
 def stream_check_error(scene, stream_ptr=None, device=0):
