@@ -614,6 +614,69 @@ struct HitInfo {
     int material;
 };
 
+// triangle_distance for the leaf round, with the nine vertex components LOADED in the ray's axis
+// order (rotation r = k0: [r, r + 1, r + 2] mod 3) -- a lane-varying address offset per axis
+// instead of two selects per 32-bit half of every component (36 v_cndmask) -- and the hit point
+// formed in the rotated axes (per component the same operations on the same values), its offset
+// from the origin rotated back before the x, y, z sum of squares: the same bits as
+// triangle_distance.  `rank`: the triangle's reference rank (TriVerts::rank).
+__device__ __forceinline__ double triangle_distance_rot(const TriVerts* t, const RayPre& p, int64_t& rank) {
+    const int k0 = p.k0(), k1 = p.k1(), k2 = p.k2();
+    const double* tv = t->v;
+    double px[3], py[3], pz[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        px[i] = tv[3 * i + k0];
+        py[i] = tv[3 * i + k1];
+        pz[i] = tv[3 * i + k2];
+    }
+    rank = t->rank;
+    const double ox = sel(p.o, k0), oy = sel(p.o, k1), oz = sel(p.o, k2);
+    double tx[3], ty[3], az[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double ax = px[i] + (-ox), ay = py[i] + (-oy);
+        az[i] = pz[i] + (-oz);
+        tx[i] = ax + p.sx * az[i];
+        ty[i] = ay + p.sy * az[i];
+    }
+    const double e0 = tx[1] * ty[2] - tx[2] * ty[1];
+    const double e1 = tx[2] * ty[0] - tx[0] * ty[2];
+    const double e2 = tx[0] * ty[1] - tx[1] * ty[0];
+    const bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
+    if (!((!s0 && !s1 && !s2) || (s0 && s1 && s2))) return -1.0;
+    const double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
+    double s = 0.0;
+    s = s + ea0;
+    s = s + ea1;
+    s = s + ea2;
+    const double inv = 1.0 / s;
+    const double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
+    double tz = 0.0;
+    tz = tz + az[0] * b0;
+    tz = tz + az[1] * b1;
+    tz = tz + az[2] * b2;
+    if (sgn(tz) != sgn(p.pdz)) return -1.0;
+    // location, rotated: component j is axis k_j (fold from zero, vertex order as triangle.rs:66-71)
+    double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+    l0 = l0 + px[0] * b0;
+    l1 = l1 + py[0] * b0;
+    l2 = l2 + pz[0] * b0;
+    l0 = l0 + px[1] * b1;
+    l1 = l1 + py[1] * b1;
+    l2 = l2 + pz[1] * b1;
+    l0 = l0 + px[2] * b2;
+    l1 = l1 + py[2] * b2;
+    l2 = l2 + pz[2] * b2;
+    const double d0 = ox - l0, d1 = oy - l1, d2 = oz - l2;  // origin - location, rotated
+    // back to x, y, z: r = 0 (d0, d1, d2), r = 1 (d2, d0, d1), r = 2 (d1, d2, d0)
+    const double dx = k0 == 0 ? d0 : (k0 == 1 ? d2 : d1);
+    const double dy = k0 == 0 ? d1 : (k0 == 1 ? d0 : d2);
+    const double dz = k0 == 0 ? d2 : (k0 == 1 ? d1 : d0);
+    const V3 dv = mk(dx, dy, dz);
+    return sqrt(dot(dv, dv));
+}
+
 // triangle_distance's barycentrics only (the winning triangle's shading, whose hit is known):
 // the same operations up to b0..b2, without tz, the location and the distance's sqrt
 __device__ __forceinline__ void triangle_bary(const TriVerts& t, const RayPre& p, double bary[3]) {

@@ -129,6 +129,9 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_LATE_BOX  // leaf round: the exact box test only for entries whose triangle hits
 #define VR_LATE_BOX 1
 #endif
+#ifndef VR_ROT_LOAD  // leaf round: vertex components loaded in the owner ray's axis order (A/B: rejected)
+#define VR_ROT_LOAD 0
+#endif
 #ifndef VR_WAVE_LEAF
 #define VR_WAVE_LEAF 1
 #endif
@@ -368,6 +371,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // only for hitting entries -- the wave runs the six f64 divisions only when such an entry
         // exists, not whenever an entry's f32 box test was too close to call.  The counting variant
         // tests every flagged box, so its counters stay the reference's.
+#if VR_ROT_LOAD
+        if (mine) {
+            // vertex components loaded in the owner ray's axis order (no per-component selects)
+            int64_t rk;
+            d = triangle_distance_rot(VR_TRIS + tri, op, rk);  // the owner's shear constants, not its direction
+            rank = (uint32_t)rk;
+            if (COUNT && e >= 0) cnt.tri_tests++;
+        }
+#else
         TriVerts tv;
         if (mine) {
             tv = load_tri(VR_TRIS + tri);
@@ -376,6 +388,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             rank = (uint32_t)tv.rank;
             if (COUNT && e >= 0) cnt.tri_tests++;
         }
+#endif
         // lanes with an entry (lane < n) whose box was too close to call (e < 0) and whose triangle
         // hits (d >= 0), as compares into lane masks
         const uint64_t flagged = __builtin_amdgcn_uicmp(lane, n, 36 /* ult */) & lanes_igt(0, e);
@@ -387,6 +400,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 VR_SEC(2);
                 VR_MARK("exact_box");
                 if (COUNT) cnt.exact_boxes++;
+#if VR_ROT_LOAD
+                const TriVerts tv = load_tri(VR_TRIS + tri);  // in x, y, z order (rare path)
+#endif
                 double bb[6], lo, hi;
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
