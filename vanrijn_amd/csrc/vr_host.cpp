@@ -15,6 +15,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -288,6 +289,10 @@ float round_upper(double v) {
     return f;
 }
 
+#ifndef VR_WIDE_DP  // 4-wide collapse: SAH-optimal DP (1) or greedy by largest child area (0)
+#define VR_WIDE_DP 1
+#endif
+
 // The render kernel's 4-wide tree, collapsed from a binary tree (the SAH traversal tree, or the
 // reference's median-split tree): starting from a binary node's two children, the interior child
 // with the largest surface area is replaced by its two children until there are four (or only
@@ -300,7 +305,8 @@ struct WideBuilder {
     const std::vector<vr::Node>& bin;
     std::vector<vr::Node4>& n4;
     int stack = 0;
-    WideBuilder(const std::vector<vr::Node>& b, std::vector<vr::Node4>& a) : bin(b), n4(a) {}
+    bool dp = false;  // the SAH-optimal DP collapse (else greedy by largest child area)
+    WideBuilder(const std::vector<vr::Node>& b, std::vector<vr::Node4>& a, bool dp_ = false) : bin(b), n4(a), dp(dp_) {}
 
     static double area(const double* b) {
         const double dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
@@ -308,16 +314,80 @@ struct WideBuilder {
         return dx * dy + dy * dz + dz * dx;
     }
 
+    // SAH-optimal collapse (VR_WIDE_DP): a visit of a wide node costs one node step whatever its
+    // children, and is entered with probability ~ its surface area, so the wide tree minimising
+    // sum(SA(wide node)) is chosen by a bottom-up DP over the binary tree (as in Ylitie et al.'s
+    // wide-BVH collapse, leaf size 1): F(x) = SA(x) + H(x, 4) is x as a wide node; C(x, k), the best
+    // cost of x's subtree in at most k slots of its parent, = min(F(x), H(x, k)) for k >= 2 (x
+    // dissolved into its children) and F(x) for k = 1; H(x, k) = min over a of C(l, a) + C(r, k - a),
+    // a leaf costing 0.  split[x][k]: 0 keeps x as one slot, a > 0 gives its left child a slots.
+    std::vector<std::array<double, 5>> C;
+    std::vector<std::array<uint8_t, 5>> split;
+    double H(int32_t x, int k, uint8_t& arg) const {
+        double best = INFINITY;
+        for (int a = 1; a < k; ++a) {
+            const int32_t l = bin[x].child[0], r = bin[x].child[1];
+            const double v = (l >= 0 ? C[l][a] : 0.0) + (r >= 0 ? C[r][k - a] : 0.0);
+            if (v < best) {
+                best = v;
+                arg = (uint8_t)a;
+            }
+        }
+        return best;
+    }
+    void plan(int32_t x, double sa) {  // x interior, sa: its surface area
+        if (C.size() < bin.size()) {
+            C.resize(bin.size());
+            split.resize(bin.size());
+        }
+        for (int c = 0; c < 2; ++c)
+            if (bin[x].child[c] >= 0) plan(bin[x].child[c], area(bin[x].box[c]));
+        uint8_t a4 = 1;
+        const double f = sa + H(x, 4, a4);
+        C[x][1] = f;
+        split[x][1] = 0;
+        for (int k = 2; k <= 4; ++k) {
+            uint8_t a = 1;
+            const double h = H(x, k, a);
+            C[x][k] = h < f ? h : f;
+            split[x][k] = h < f ? a : 0;
+        }
+        split[x][0] = a4;  // the split of x's two children over a wide node's 4 slots
+    }
+    void plan_root(int32_t b) {  // before collapse(b, 0) of a BVH root
+        double u[6];
+        for (int j = 0; j < 6; ++j)
+            u[j] = (j & 1) ? std::max(bin[b].box[0][j], bin[b].box[1][j]) : std::min(bin[b].box[0][j], bin[b].box[1][j]);
+        plan(b, area(u));
+    }
+    void expand(int32_t x, const double* bx, int k, int32_t* code, const double** box, int& n) const {
+        if (x < 0 || k == 1 || split[x][k] == 0) {
+            code[n] = x;
+            box[n] = bx;
+            ++n;
+            return;
+        }
+        expand(bin[x].child[0], bin[x].box[0], split[x][k], code, box, n);
+        expand(bin[x].child[1], bin[x].box[1], k - split[x][k], code, box, n);
+    }
+
     // wide node over binary interior node `b`; `pushed`: stack entries held by its ancestors
     int32_t collapse(int32_t b, int pushed) {
         int32_t code[4];
         const double* box[4];
         int n = 2;
-        for (int c = 0; c < 2; ++c) {
-            code[c] = bin[b].child[c];
-            box[c] = bin[b].box[c];
+        if (dp) {
+            n = 0;
+            const int a = split[b][0];
+            expand(bin[b].child[0], bin[b].box[0], a, code, box, n);
+            expand(bin[b].child[1], bin[b].box[1], 4 - a, code, box, n);
+        } else {
+            for (int c = 0; c < 2; ++c) {
+                code[c] = bin[b].child[c];
+                box[c] = bin[b].box[c];
+            }
         }
-        while (n < 4) {
+        while (!dp && n < 4) {
             int pick = -1;
             double best = -1.0;
             for (int k = 0; k < n; ++k)
@@ -729,11 +799,46 @@ int hot_prefix(std::vector<vr::Node4>& n4, std::vector<vr::Bvh>& bvhs, int k) {
 
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
-    s->nodes4.clear();
-    WideBuilder W(nodes, s->nodes4);
-    for (auto& b : s->bvhs) b.root4 = b.root >= 0 ? W.collapse(b.root, 0) : b.root;
-    s->wide_stack = W.stack;
+    // greedy collapse; with VR_WIDE_DP the SAH-optimal one instead, unless its (deeper) stack bound
+    // would move the kernel to a larger LDS stack class (24 / 32 / 48 entries: fewer workgroups)
+    auto stack_class = [](int st) { return st + 1 <= 24 ? 0 : (st + 1 <= 32 ? 1 : 2); };
+    std::vector<vr::Node4> greedy;
+    WideBuilder G(nodes, greedy, false);
+    std::vector<int32_t> groot(s->bvhs.size());
+    for (size_t i = 0; i < s->bvhs.size(); ++i)
+        groot[i] = s->bvhs[i].root >= 0 ? G.collapse(s->bvhs[i].root, 0) : s->bvhs[i].root;
+    bool use_dp = false;
+    std::vector<vr::Node4> opt;
+    std::vector<int32_t> oroot(s->bvhs.size());
+    int ostack = 0;
+    if (VR_WIDE_DP && !(getenv("VR_WIDE_DP") && atoi(getenv("VR_WIDE_DP")) == 0)) {
+        WideBuilder D(nodes, opt, true);
+        for (size_t i = 0; i < s->bvhs.size(); ++i) {
+            if (s->bvhs[i].root >= 0) D.plan_root(s->bvhs[i].root);
+            oroot[i] = s->bvhs[i].root >= 0 ? D.collapse(s->bvhs[i].root, 0) : s->bvhs[i].root;
+        }
+        ostack = D.stack;
+        use_dp = stack_class(D.stack) <= stack_class(G.stack);
+    }
+    s->nodes4 = use_dp ? std::move(opt) : std::move(greedy);
+    for (size_t i = 0; i < s->bvhs.size(); ++i) s->bvhs[i].root4 = use_dp ? oroot[i] : groot[i];
+    s->wide_stack = use_dp ? ostack : G.stack;
     s->wide_count = s->nodes4.size();
+    if (getenv("VR_WIDE_STATS")) {  // diagnostic: the collapse's SAH objective, sum SA(wide) / SA(root)
+        double sum = 0.0, root = 0.0;
+        for (const auto& w : s->nodes4) {
+            float u[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
+            for (int k = 0; k < 4; ++k)
+                if (w.child[k] != vr::kEmptyChild)
+                    for (int j = 0; j < 6; ++j) u[j] = (j & 1) ? std::max(u[j], w.box[k][j]) : std::min(u[j], w.box[k][j]);
+            const double a = (double)(u[1] - u[0]) * (u[3] - u[2]) + (double)(u[3] - u[2]) * (u[5] - u[4]) +
+                             (double)(u[5] - u[4]) * (u[1] - u[0]);
+            sum += a;
+            if (&w == &s->nodes4[0]) root = a;
+        }
+        std::fprintf(stderr, "vr wide tree: %zu nodes, stack %d, sum SA / SA(first root) %.4f (%s collapse)\n",
+                     s->nodes4.size(), s->wide_stack, sum / root, use_dp ? "DP" : "greedy");
+    }
     s->dev.hot_count = hot_prefix(s->nodes4, s->bvhs, hot_node_budget());
 }
 
