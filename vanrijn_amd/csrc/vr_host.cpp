@@ -159,6 +159,9 @@ struct BvhBuilder {
     }
 };
 
+#ifndef VR_SAH_BINS  // bins per axis of the host's binned SAH (the device build uses 32)
+#define VR_SAH_BINS 32
+#endif
 // Traversal tree (the default): a binned-SAH binary tree over the same triangles, leaf size 1.
 // The reference's closest hit does not depend on its tree: a box test on a superset box passes
 // whenever it passes on the subset (every rounding step of (bound - o) / d is monotonic in
@@ -187,7 +190,7 @@ struct SahBuilder {
                 cmin[c] = std::min(cmin[c], prims[i].centre[c]);
                 cmax[c] = std::max(cmax[c], prims[i].centre[c]);
             }
-        constexpr int kBins = 32;
+        constexpr int kBins = VR_SAH_BINS;
         int best_axis = -1, best_bin = -1;
         double best_cost = INFINITY;
         // median splits where SAH would push the tree past the deepest traversal stack (48)
