@@ -375,22 +375,21 @@ struct WideBuilder {
     }
 
     // wide node over binary interior node `b`; `pushed`: stack entries held by its ancestors
-    int32_t collapse(int32_t b, int pushed) {
-        int32_t code[4];
-        const double* box[4];
-        int n = 2;
-        if (dp) {
-            n = 0;
+    // the children of a wide node over binary node b: the DP's expansion or the greedy one
+    int children(int32_t b, bool use_dp, int32_t* code, const double** box) const {
+        int n = 0;
+        if (use_dp) {
             const int a = split[b][0];
             expand(bin[b].child[0], bin[b].box[0], a, code, box, n);
             expand(bin[b].child[1], bin[b].box[1], 4 - a, code, box, n);
-        } else {
-            for (int c = 0; c < 2; ++c) {
-                code[c] = bin[b].child[c];
-                box[c] = bin[b].box[c];
-            }
+            return n;
         }
-        while (!dp && n < 4) {
+        for (int c = 0; c < 2; ++c) {
+            code[c] = bin[b].child[c];
+            box[c] = bin[b].box[c];
+        }
+        n = 2;
+        while (n < 4) {
             int pick = -1;
             double best = -1.0;
             for (int k = 0; k < n; ++k)
@@ -406,6 +405,35 @@ struct WideBuilder {
             box[n] = c.box[1];
             ++n;
         }
+        return n;
+    }
+    // stack bound of the wide subtree over b when every node below uses the DP (or the greedy)
+    // expansion: (interior children - 1) + the deepest child's (memoised)
+    std::vector<int16_t> need_memo[2];
+    int need(int32_t b, bool use_dp) {
+        auto& m = need_memo[use_dp];
+        if (m.size() < bin.size()) m.assign(bin.size(), -1);
+        if (m[b] >= 0) return m[b];
+        int32_t code[4];
+        const double* box[4];
+        const int n = children(b, use_dp, code, box);
+        int interior = 0, deepest = 0;
+        for (int k = 0; k < n; ++k)
+            if (code[k] >= 0) {
+                ++interior;
+                deepest = std::max(deepest, need(code[k], use_dp));
+            }
+        return m[b] = (int16_t)(std::max(0, interior - 1) + deepest);
+    }
+    int limit = 1 << 30;  // dp: a node takes the DP expansion only if its DP subtree's stack fits
+
+    // wide node over binary interior node `b`; `pushed`: stack entries held by its ancestors
+    int32_t collapse(int32_t b, int pushed) {
+        int32_t code[4];
+        const double* box[4];
+        // the DP expansion where its whole subtree's stack bound fits under `limit` from here (then
+        // it fits at every node below too); else greedy here, and the children decide for themselves
+        const int n = children(b, dp && pushed + need(b, true) <= limit, code, box);
         const int32_t me = (int32_t)n4.size();
         n4.emplace_back();
         int interior = 0;
@@ -802,9 +830,10 @@ int hot_prefix(std::vector<vr::Node4>& n4, std::vector<vr::Bvh>& bvhs, int k) {
 
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
-    // greedy collapse; with VR_WIDE_DP the SAH-optimal one instead, unless its (deeper) stack bound
-    // would move the kernel to a larger LDS stack class (24 / 32 / 48 entries: fewer workgroups)
-    auto stack_class = [](int st) { return st + 1 <= 24 ? 0 : (st + 1 <= 32 ? 1 : 2); };
+    // greedy collapse; with VR_WIDE_DP the SAH-optimal one instead wherever its (deeper) stack
+    // bound keeps the kernel in the greedy tree's LDS stack class (24 / 32 / 48 entries; a larger
+    // class would cost workgroups per CU): a node takes the DP expansion when its DP subtree fits
+    auto class_limit = [](int st) { return st + 1 <= 24 ? 23 : (st + 1 <= 32 ? 31 : 47); };
     std::vector<vr::Node4> greedy;
     WideBuilder G(nodes, greedy, false);
     std::vector<int32_t> groot(s->bvhs.size());
@@ -816,12 +845,13 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     int ostack = 0;
     if (VR_WIDE_DP && !(getenv("VR_WIDE_DP") && atoi(getenv("VR_WIDE_DP")) == 0)) {
         WideBuilder D(nodes, opt, true);
+        D.limit = class_limit(G.stack);
         for (size_t i = 0; i < s->bvhs.size(); ++i) {
             if (s->bvhs[i].root >= 0) D.plan_root(s->bvhs[i].root);
             oroot[i] = s->bvhs[i].root >= 0 ? D.collapse(s->bvhs[i].root, 0) : s->bvhs[i].root;
         }
         ostack = D.stack;
-        use_dp = stack_class(D.stack) <= stack_class(G.stack);
+        use_dp = D.stack <= D.limit;  // (by construction)
     }
     s->nodes4 = use_dp ? std::move(opt) : std::move(greedy);
     for (size_t i = 0; i < s->bvhs.size(); ++i) s->bvhs[i].root4 = use_dp ? oroot[i] : groot[i];
