@@ -1402,6 +1402,9 @@ __global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask
     if (tid == 1023) *count = part[1023];
 }
 
+#ifndef VR_REDUCE_BATCH  // samples whose colours the ordered reduce computes together
+#define VR_REDUCE_BATCH 4
+#endif
 typedef double d2 __attribute__((ext_vector_type(2)));
 // accumulation_buffer.rs:44-60 (update_pixel with weight 1.0), one thread per pixel, samples in
 // order: the same Kahan sequence the reference applies call by call.
@@ -1439,7 +1442,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     };
     // the colours of kB samples are independent (7 exp() each): computed together, then folded in
     // order -- the same operations as one at a time, with kB-fold instruction-level parallelism
-    constexpr uint32_t kB = 4;
+    constexpr uint32_t kB = VR_REDUCE_BATCH;
     uint32_t s = 0;
     if (mask) {
         const uint64_t py = p / tile_width, px = p - py * tile_width;
