@@ -28,8 +28,7 @@ def main():
     os.environ["VR_WG_TIMES_PATH"] = path
     cnt = render_tile_device(ds, Tile(0, W, 0, H), H, W, spp, 1, 0, state.data_ptr(), stream, counters=True)
     del os.environ["VR_WG_TIMES_PATH"]
-    raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 16)  # per workgroup: vr_layout.h kWgTimeWords
-    t = raw[:, :2].astype(np.float64) * 10.0  # ns
+    t = np.fromfile(path, dtype=np.uint64).reshape(-1, 2).astype(np.float64) * 10.0  # ns
     s, e = t[:, 0] - t[:, 0].min(), t[:, 1] - t[:, 0].min()
     rec = render_samples(ds, Tile(0, W, 0, H), H, W, spp, seed=1)
     b = rec["bounces"].reshape(-1)
@@ -42,17 +41,6 @@ def main():
                        "max": int(b.max()), "paths_ge_64": int((b >= 64).sum()), "paths_at_128": int((b >= 128).sum())},
            "lane_utilisation": {"traversal": cnt["node_visits"] / max(1, cnt["traversal_slots"]),
                                 "path_loop": cnt["rays"] / max(1, cnt["path_loop_slots"])}}
-    # per wave (4 per workgroup): end time, its longest path's bounces, its paths of >= 64 bounces
-    wv = raw[:, 2:14].reshape(-1, 4, 3)
-    wend = (wv[:, :, 0].astype(np.float64) * 10.0 - t[:, 0].min()).reshape(-1)
-    wmax = wv[:, :, 1].reshape(-1).astype(np.int64)
-    wlong = wv[:, :, 2].reshape(-1).astype(np.int64)
-    order = np.argsort(-wend)[:12]
-    out["slowest_waves"] = [{"end_ms": round(float(wend[i] / 1e6), 3), "max_bounces": int(wmax[i]),
-                             "long_paths": int(wlong[i])} for i in order]
-    out["waves_by_long_paths"] = {int(k): {"waves": int((wlong == k).sum()),
-                                           "end_ms_max": round(float(wend[wlong == k].max() / 1e6), 3)}
-                                  for k in np.unique(wlong)}
     print(json.dumps(out), flush=True)
 
 

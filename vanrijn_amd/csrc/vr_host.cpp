@@ -1087,23 +1087,10 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = getenv("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
-    // the cooperative tail (vr_render.hip coop_step): launches of at most VR_COOP_SAMPLES (4 M)
-    // pixel-samples, whose time is their longest paths' (C1, one sample of a 1024^2 frame); large
-    // launches keep the kernel without it (its registers spill a little).  VR_COOP=0 / 1 / 2 forces
-    // it off / one owner per wave / up to two.
-    const uint64_t lsamples = (p->tile.end_column - p->tile.start_column) * (p->tile.end_row - p->tile.start_row) *
-                              (uint64_t)p->spp;
-    const char* cs = getenv("VR_COOP_SAMPLES");
-    const uint64_t coop_max = cs ? (uint64_t)std::max(0LL, atoll(cs)) : (4ull << 20);
+    // tuning hook (A/B): 0 turns the cooperative tail off in a build compiled with -DVR_COOP=1
+    // (the default build compiles it out: rejected, vr_render.hip)
     const char* co = getenv("VR_COOP");
-    a.coop = co ? (uint32_t)std::min(2, std::max(0, atoi(co))) : (lsamples <= coop_max ? 2u : 0u);  // owners served
-    // only paths that have bounced this often: 48, beyond any path of the main.rs scene (its longest
-    // are 24-33 bounces) -- a path trapped between mirrors (the bench scene's creases run to the
-    // 128-bounce limit).  The breadth-first walk over the lanes pushes children unsorted, so a ray
-    // without an early near hit visits most of what its line crosses: measured on main.rs's 1-spp
-    // frame with 8, paths of 9-21 bounces took 5-13 ms (profiles/r03/ad/)
-    const char* cb = getenv("VR_COOP_BOUNCES");
-    a.coop_bounces = cb ? (uint32_t)std::max(0, atoi(cb)) : 48u;
+    a.coop = co ? (uint32_t)(atoi(co) != 0) : 1u;
     const char* lf = getenv("VR_LEAF_FEW");  // tuning hook (0: off)
     a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;
     const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
@@ -1819,10 +1806,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         lock.lock();
         VR_HIP(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long) * vr::kCntCount, st));
         counters = s->d_counters;
-        if (wg_path) {
-            VR_HIP(hipMalloc(&wg.ptr, blocks * vr::kWgTimeWords * sizeof(unsigned long long)));
-            VR_HIP(hipMemsetAsync(wg.ptr, 0, blocks * vr::kWgTimeWords * sizeof(unsigned long long), st));
-        }
+        if (wg_path) VR_HIP(hipMalloc(&wg.ptr, blocks * 2 * sizeof(unsigned long long)));
     }
     PassEvents pe;
     {
@@ -1872,7 +1856,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
             }
         }
         if (wg_path && wg.ptr) {
-            std::vector<unsigned long long> t(blocks * vr::kWgTimeWords);
+            std::vector<unsigned long long> t(blocks * 2);
             VR_HIP(hipMemcpy(t.data(), wg.ptr, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
             if (FILE* f = std::fopen(wg_path, "wb")) {
                 std::fwrite(t.data(), sizeof(unsigned long long), t.size(), f);

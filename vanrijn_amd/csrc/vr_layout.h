@@ -10,7 +10,6 @@
 namespace vr {
 
 constexpr int kRecursionLimit = 128;       // camera.rs:69
-constexpr int kWgTimeWords = 16;           // diagnostic wg_times record per workgroup (u64 words)
 constexpr int kMaxSpectrumSamples = 64;
 constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
 // LDS copy of the top of the 4-wide tree (DeviceScene::hot_count nodes, at most kHotNodesMax:
@@ -157,11 +156,8 @@ struct RenderArgs {
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     uint32_t leaf_few;            // ... or at most this many lanes are still traversing
-    uint32_t coop;                // the launch's tail: a wave's last 1 (or up to 2) paths walk their trees
-                                  // with the wave's lanes (COOP instantiations; 0: off)
-    uint32_t coop_bounces;        // ... once each of them has bounced at least this often (trapped paths)
+    uint32_t coop;                // 1: a wave's last path walks its tree with all lanes (the launch's tail)
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
-    int32_t pad_coop;
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
     // 1: a path whose throughput and affine term are both 0 ends early (its intensity is 0 for
@@ -179,7 +175,7 @@ struct RenderArgs {
     double* state;                // [tile pixels][8]
     void* records;             // vr_sample_record* (record variant) or nullptr
     unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
-    unsigned long long* wg_times;  // counting variant: [blocks][kWgTimeWords] (vr_render.hip), or nullptr
+    unsigned long long* wg_times;  // counting variant: [blocks][2] s_memrealtime at start / end, or nullptr
     int32_t* error_flag;          // this call's error word (a singular shading basis sets it)
     // per 8x8 pixel block of the tile: 1 when every camera ray through the block provably misses
     // every object (block_cull_kernel), so each of its samples is photon {0, 0}; nullptr: none

@@ -145,14 +145,11 @@ constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
 #ifndef VR_LEAF_SKIP  // node step: skip the FIFO append when no lane met a leaf
 #define VR_LEAF_SKIP 1
 #endif
-// the launch's tail: a wave's last one or two paths walk their trees with the wave's lanes
-// (coop_step; the COOP instantiations, chosen per launch by RenderArgs::coop: small launches only).
-// Measured and rejected, compiled out unless -DVR_COOP=1: the one-owner form
-// made a lone path 1.9x faster but C1 gained 2.5 % -- C1's tail is set by the waves holding TWO
-// 128-bounce paths (profiles/r03/z/); the two-owner form cuts C1 4.5 -> 3.2 ms, but its breadth-
-// first walk pushes children unsorted, so paths without an early near hit (main.rs's 9-21-bounce
-// paths) visit most of what their line crosses (waves of 5-13 ms, profiles/r03/ad/); gated at 48
-// bounces C1 gains 9 % while the COOP kernel's spills cost main.rs's 1-spp frame 10 %.
+// the launch's tail: a wave's last path walks its tree with every lane (RenderArgs::coop).  Parity-
+// green and the lone path 1.9x faster (profiles/r03/longpath_coop.jsonl), but rejected: inside the
+// node step main +5 %, C5 +9 % (profiles/r03/ab_coop_in_node_step.txt); as a tail-only call main
+// +1.5 %, C5 +6.7 %, bench scene +2 %, while C1 gains only 2.5 % -- its long paths share waves, so
+// one live lane per wave is rare (profiles/r03/ab_coop.txt, small_frames_coop.jsonl)
 #ifndef VR_COOP
 #define VR_COOP 0
 #endif
@@ -193,8 +190,7 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          bool COOP = false>
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -213,8 +209,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     __shared__ uint8_t wl_own[4 * kWaveList];
     __shared__ unsigned long long lr_d[256], lr_key[256];  // key: rank << 32 | triangle
     __shared__ uint32_t lr_cnt[256];
-    // cooperative tail (COOP instantiations, small launches): an owner's stack column map (coop_step)
-    __shared__ uint32_t coop_map[COOP ? 256 : 1];
     const int wbase = (threadIdx.x >> 6) * kWaveList;
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
 #else
@@ -235,7 +229,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
     lr_key[tid] = 0;
     lr_cnt[tid] = 0;
-    if (COOP) coop_map[tid] = 0;
 #endif
     DeviceScene S = A.scene;
     S.prims = g_prims;
@@ -259,10 +252,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         tprev = t_;                                           \
     }
     uint32_t samples_done = 0;
-    // wg_times, per workgroup kWgTimeWords u64: [0] start, [1] end (s_memrealtime), then per wave w
-    // [2 + 3w] its end, [3 + 3w] its longest path's bounces, [4 + 3w] its paths of >= 64 bounces
-    if (COUNT && A.wg_times && tid == 0) A.wg_times[kWgTimeWords * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    uint32_t max_bounces = 0, long_paths = 0;  // counting variant with wg_times: this lane's finished paths
+    if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
     // work items run over the live blocks only (frustum-culled blocks are not in the item space)
     const uint32_t nlive = A.live_blocks ? __builtin_amdgcn_readfirstlane(*A.live_count) : bw * bh;
@@ -274,7 +264,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     const uint64_t npix = A.tile_width * A.tile_height;
     uint32_t px = 0, py = 0, s_end = 0;
     int state = kNeedRay;  // with s_idx == s_end: needs a work item
-    bool coop_on = false;  // COOP: this wave's tail walks its last paths cooperatively (sticky)
     uint32_t s_idx = 0;
     uint64_t w_next = 0, w_end = 0;  // this wave's slice of the queue (grab > 0)
     Rng rng;
@@ -623,11 +612,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             rec->bounces = bounces;
             rec->flags = flags;
         }
-        if (COUNT) {
-            samples_done++;
-            max_bounces = max(max_bounces, (uint32_t)bounces);
-            long_paths += bounces >= 64 ? 1u : 0u;
-        }
+        if (COUNT) samples_done++;
         ++s_idx;
         state = kNeedRay;
     };
@@ -803,90 +788,54 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         state = kRayReady;
     };
 
-#if VR_WAVE_LEAF
-    // The launch's tail: the queue is exhausted and one or two paths are left in the wave (a long
-    // path -- e.g. 128 mirror bounces in a crease of the reflective bench scene -- makes a small
-    // frame's time; long paths cluster in creases, so a wave may hold two).  Their walks are spread
-    // over the wave's lanes (VR_COOP): with one owner every lane works for it, with two the lower
-    // half of the lanes works for the lower owner and the upper half for the other.  Each step takes
-    // the owner's current node and up to (workers - 1) entries from the top of its stack, one per
-    // worker lane, tests them against the owner's ray, pushes the hit interior children back and
-    // queues the hit leaves for the owner.  An owner's stack spans extra lane columns of the wave
-    // (the other lanes are done): with one owner from the start, the next columns in turn; once two
-    // owners have shared the wave (coop_map, sticky for the rest of the launch), each owner keeps its
-    // own column plus the lanes of its half other than the two owners', so the map never changes
-    // under an owner whose partner finishes first.  Culling and the order-independent leaf rounds
-    // keep the closest hit and its tie rule: only the visiting order changes.
-    // Called with the whole wave active; `live` holds the one or two live lanes.
-    // the LDS word of virtual stack entry v of owner o whose column map is om (coop_map)
-    auto coop_vaddr = [&](int o, uint32_t om, int v) {
-        const int j = v / STACK, og = (int)(om & 3) - 1, op = (int)(om >> 8);
-        int col;
-        if (j == 0) {
-            col = o;
-        } else if (og < 0) {
-            col = (o + j) & 63;
-        } else {  // the (j-1)-th lane of half og that is neither owner
-            const int s1 = o < op ? o : op, s2 = o < op ? op : o, lo = og * 32;
-            col = lo + j - 1;
-            if (s1 >= lo && s1 < lo + 32 && col >= s1) ++col;
-            if (s2 >= lo && s2 < lo + 32 && col >= s2) ++col;
-        }
-        return (v % STACK) * 256 + (tid & ~63) + col;
-    };
-    auto coop_step = [&](const uint64_t live) {
+#if VR_COOP && VR_WAVE_LEAF
+    // The launch's tail: the queue is exhausted and one path is left in the wave (a long path --
+    // e.g. 128 mirror bounces in a crease of the reflective bench scene -- makes a small frame's
+    // time).  Its walk is spread over the wave's lanes (VR_COOP): each step takes the current node
+    // and up to 63 entries from the top of the owner's stack, one per lane, tests them against the
+    // owner's ray, pushes the hit interior children back and queues the hit leaves for the owner;
+    // the stack spans every lane's column of the wave (the other lanes are done).  Culling and the
+    // order-independent leaf rounds keep the closest hit and its tie rule:
+    // only the visiting order changes.  Called with the whole wave active, owner wave-uniform; the
+    // main loop's node step pays one scalar branch for it.
+    auto coop_step = [&](const int owner) {
         uint32_t lmask = 0;
         int32_t lent[4];
-        const int oa = (int)__builtin_ctzll(live);         // lower owner
-        const int ob = (int)(63 - __builtin_clzll(live));  // upper owner (== oa: one owner)
-        const bool two = oa != ob;
-        uint32_t* cmap = &coop_map[tid & ~63];  // per lane: 0 (full map), or 1 + half | partner << 8
-        if (two && cmap[oa] == 0) {
-            if ((int)lane == oa) cmap[oa] = 1u | ((uint32_t)ob << 8);
-            if ((int)lane == ob) cmap[ob] = 2u | ((uint32_t)oa << 8);
-        }
-        // this lane works for its half's owner (two owners) or the one owner
-        const bool upper = two && lane >= 32;
-        const int owner = upper ? ob : oa;
-        const int gbase = upper ? 32 : 0, gsize = two ? 32 : 64;
-        const uint64_t gmask = two ? (upper ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
-        const int r = (int)lane - gbase;  // worker rank
-        const uint32_t om = cmap[owner];  // the owner's column map
-        const int o_sp = __shfl(sp, owner);
-        const int o_node = __shfl(node, owner);
-        const bool o_trav = __shfl(state == kTraversing ? 1 : 0, owner) != 0;
+        const int o_sp = __builtin_amdgcn_readlane(sp, owner);
+        const int o_node = __builtin_amdgcn_readlane(node, owner);
+        const bool o_trav = __builtin_amdgcn_readlane(state == kTraversing ? 1 : 0, owner) != 0;
         const int have = o_trav ? (o_node >= 0 ? 1 : 0) + o_sp : 0;
-        // the owner's stack capacity: every column of the wave, or its own plus 30 of its half
-        const int cap = ((om & 3) == 0 ? 64 : 31) * STACK;
-        // entries taken this step: at most one per worker, and at most what keeps 150 entries of
-        // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a near-full
-        // stack needs at most 3 per level below)
-        int t = have < gsize ? have : gsize;
-        const int room = (cap - 150 - have) / 3;
+        constexpr int kCap = 64 * STACK;  // the big stack: every lane column of the wave
+        // entries taken this step: at most 64, and at most what keeps 150 entries of
+        // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a
+        // near-full stack needs at most 3 per level below)
+        int t = have < 64 ? have : 64;
+        const int room = (kCap - 150 - have) / 3;
         if (t > room) t = room < 1 ? (have > 0 ? 1 : 0) : room;
-        const bool work = t > 0 && VR_ROOM;  // uniform per half
-        uint32_t im = 0;                     // hit interior children
-        int c[4] = {0, 0, 0, 0};
-        int pos = o_sp;
-        if (work) {
+        if (t > 0 && VR_ROOM) {
             VR_MARK("coop_step");
-            const int first_stack = o_node >= 0 ? 1 : 0;  // worker 0 takes the current node
+            // virtual stack index v of the owner -> its LDS word: v < STACK is the owner's own
+            // column (the usual layout), then the next lanes' columns in turn
+            auto vaddr = [&](int v) { return (v % STACK) * 256 + (tid & ~63) + ((owner + v / STACK) & 63); };
+            const int first_stack = o_node >= 0 ? 1 : 0;  // lane 0 takes the current node
             int my = -1;
-            if (r < t) my = (r < first_stack) ? o_node : (int)st_node[coop_vaddr(owner, om, o_sp - 1 - (r - first_stack))];
-            pos = o_sp - (t - first_stack);  // stack entries left below the taken ones
-            Ray32 ry;                        // the owner's ray and cull bounds
-            ry.ox = __shfl(pre32.ox, owner);
-            ry.oy = __shfl(pre32.oy, owner);
-            ry.oz = __shfl(pre32.oz, owner);
-            ry.ix = __shfl(pre32.ix, owner);
-            ry.iy = __shfl(pre32.iy, owner);
-            ry.iz = __shfl(pre32.iz, owner);
-            ry.nx = __shfl(pre32.nx, owner);
-            ry.ny = __shfl(pre32.ny, owner);
-            ry.nz = __shfl(pre32.nz, owner);
-            ry.ek = __shfl(pre32.ek, owner);
-            const float cf = __shfl(cull_far, owner);
-            const float cb = __shfl(cull_behind, owner);
+            if ((int)lane < t) my = ((int)lane < first_stack) ? o_node : (int)st_node[vaddr(o_sp - 1 - ((int)lane - first_stack))];
+            const int base = o_sp - (t - first_stack);  // stack entries left below the taken ones
+            Ray32 r;  // the owner's ray and cull bounds, wave-uniform
+            r.ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ox), owner));
+            r.oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oy), owner));
+            r.oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oz), owner));
+            r.ix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ix), owner));
+            r.iy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iy), owner));
+            r.iz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iz), owner));
+            r.nx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nx), owner));
+            r.ny = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ny), owner));
+            r.nz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nz), owner));
+            r.ek = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ek), owner));
+            const float cf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_far), owner));
+            const float cb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_behind), owner));
+            uint32_t im = 0;  // hit interior children
+            int c[4];
             if (my >= 0) {
                 const Node4& nd = VR_NODES4[my];
                 if (COUNT) cnt.node_visits++;
@@ -896,7 +845,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     c[k] = nd.child[k];
                     float f, g;
                     bool maybe, sure;
-                    slab32_flags(nd.box[k], ry, f, g, maybe, sure);
+                    slab32_flags(nd.box[k], r, f, g, maybe, sure);
                     const bool lv = c[k] != kEmptyChild;
                     if (COUNT && lv) cnt.box_tests++;
                     const bool pass = lv && maybe && !(f > cf || g < cb);
@@ -906,43 +855,38 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
                 }
             }
-        }
-        // interior hits onto the owner's stack, in (child slot, worker) order
+            // interior hits onto the owner's stack, in (child slot, lane) order
+            int pos = base;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool ih = (im >> k) & 1u;
-            const uint64_t m = __ballot(ih) & gmask;
-            if (ih) st_node[coop_vaddr(owner, om, pos + (int)lanes_below(m))] = (uint32_t)c[k];
-            pos += (int)__popcll(m);
-        }
-        // each owner takes its next node, the top of its stack: its workers' pos and work flag
-        // (uniform over its half) by permute from the half's first lane
-        const int lead = (two && (int)lane == ob) ? 32 : 0;
-        const int npos = __shfl(pos, lead);
-        const bool nwork = __shfl(work ? 1 : 0, lead) != 0;
-        const bool is_owner = ((live >> lane) & 1ull) != 0;
-        if (is_owner && nwork) {
-            sp = npos;
-            if (sp > 0) {
-                --sp;
-                node = (int)st_node[coop_vaddr((int)lane, cmap[lane], sp)];
-            } else {
-                node = -1;
+            for (int k = 0; k < 4; ++k) {
+                const bool ih = (im >> k) & 1u;
+                const uint64_t m = __ballot(ih);
+                if (ih) st_node[vaddr(pos + (int)lanes_below(m))] = (uint32_t)c[k];
+                pos += (int)__popcll(m);
+            }
+            // the owner's next node: the top of its stack
+            if ((int)lane == owner) {
+                sp = pos;
+                if (sp > 0) {
+                    --sp;
+                    node = (int)st_node[vaddr(sp)];
+                } else {
+                    node = -1;
+                }
             }
         }
-        // the hit leaves, queued for their owners in (child slot, lane) order
-        const uint64_t own_mask = two ? ((int)lane == ob ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
+        // the hit leaves, queued for the owner in (child slot, lane) order
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const bool lh = (lmask >> k) & 1u;
             const uint64_t m = __ballot(lh);
             if (lh) {
-                const uint32_t qp = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
-                wl_tri[wbase + qp] = lent[k];
-                wl_own[wbase + qp] = (uint8_t)owner;
+                const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
+                wl_tri[wbase + pos] = lent[k];
+                wl_own[wbase + pos] = (uint8_t)owner;
             }
             q_tail += (uint32_t)__popcll(m);
-            if (is_owner) np += (int)__popcll(m & own_mask);
+            if ((int)lane == owner) np += (int)__popcll(m);
         }
         q_tail = __builtin_amdgcn_readfirstlane(q_tail);
     };
@@ -1132,20 +1076,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const int n = VR_ROOM ? __popcll(lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) : 0;
                 if (first_active_lane()) step_hist[n == 0 ? 0 : 1 + (n - 1) / 8]++;
             }
-#if VR_WAVE_LEAF
-            if (COOP && A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
+#if VR_COOP && VR_WAVE_LEAF
+            if (A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
                 const uint64_t live = __ballot(state != kDone);
-                const int nlive = __popcll(live);
-                // A.coop: owners served (1 or 2); to start, every live path must have bounced
-                // A.coop_bounces times (a path trapped in a crease: short tails keep the depth-first
-                // walk).  Once on, it stays on for the wave: an owner's stack may span other lanes'
-                // columns, and the live set only shrinks (a live lane may still start a new path from
-                // the wave's slice, with its own empty stack)
-                if (!coop_on)
-                    coop_on = nlive >= 1 && nlive <= (int)A.coop &&
-                              (__ballot(state != kDone && bounces >= (int)A.coop_bounces) == live);
-                coop = coop_on && nlive >= 1;
-                if (coop) coop_step(live);
+                coop = __popcll(live) == 1;
+                if (coop) coop_step((int)__builtin_ctzll(live));
             }
 #endif
             if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
@@ -1336,13 +1271,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (step_hist[i]) atomicAdd(&A.counters[kCntStepHist + i], (unsigned long long)step_hist[i]);
         }
         if (A.wg_times) {
-            unsigned long long* wg = A.wg_times + kWgTimeWords * blockIdx.x;
-            const int w = tid >> 6;
-            if (first_active_lane()) wg[2 + 3 * w] = __builtin_amdgcn_s_memrealtime();
-            atomicMax(&wg[3 + 3 * w], (unsigned long long)max_bounces);
-            if (long_paths) atomicAdd(&wg[4 + 3 * w], (unsigned long long)long_paths);
             __syncthreads();
-            if (tid == 0) wg[1] = __builtin_amdgcn_s_memrealtime();
+            if (tid == 0) A.wg_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
@@ -1647,10 +1577,6 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
 #define VR_LAUNCH(C, R, D, M, W)                                                                      \
     hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a, a.scene.prims, \
                        a.scene.materials, a.scene.bvhs)
-    // the cooperative-tail instantiations: launches the host marks small (RenderArgs::coop)
-#define VR_LAUNCH_COOP(C, D, M)                                                                            \
-    hipLaunchKernelGGL((dev::render_kernel<STACK, C, false, D, M, 3, false, true>), grid, block, 0, s, a, \
-                       a.scene.prims, a.scene.materials, a.scene.bvhs)
 #ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
@@ -1660,19 +1586,10 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     else if (variant == 4) VR_LAUNCH(false, false, D, M, 4); \
     else VR_LAUNCH(false, false, D, M, 3)
 #else
-#if VR_COOP
-#define VR_MODES(D, M)                                     \
-    if (recording) VR_LAUNCH(false, true, D, M, 3);        \
-    else if (counting && a.coop) VR_LAUNCH_COOP(true, D, M); \
-    else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
-    else if (a.coop) VR_LAUNCH_COOP(false, D, M);          \
-    else VR_LAUNCH(false, false, D, M, 3)
-#else
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
     else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
     else VR_LAUNCH(false, false, D, M, 3)
-#endif
 #endif
     if (!dark0) {
         VR_MODES(false, 3);
