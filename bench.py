@@ -568,7 +568,7 @@ def main():
                      "ms_per_step": round(sum(rccl_ms) / len(rccl_ms), 3) if rccl_ms else 0.0}
     out["roofline"]["reduce_kernel_ms"] = round(sum(reduce_ms) / len(reduce_ms), 3)
     # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied
-    # as the photon {0, 0} without tracing: the records are bit-identical with VR_BLOCK_CULL=0
+    # as the photon {0, 0} without tracing: the records are bit-identical with VR_LAUNCH_NO_CULL
     # (tests/test_gpu_cull.py); every sample is counted in `value`
     out["roofline"]["frustum_culled_sample_fraction"] = round(1.0 - counts["samples"] / (W * H * spp), 4)
     if rank == 0 and world == 1 and not args.no_drop_in:

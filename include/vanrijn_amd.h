@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 6
+#define VR_ABI_VERSION 7
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -167,6 +167,10 @@ typedef struct vr_scene vr_scene;
  * scene's; only the build time differs.  Implies VR_SCENE_DEVICE_BVH; ignored with
  * VR_SCENE_REFERENCE_BVH or VR_SCENE_HOST_ONLY. */
 #define VR_SCENE_DEVICE_SAH 8u
+/* Collapse the binary traversal tree to the 4-wide render tree greedily (the largest-area interior
+ * child expanded first) instead of by the SAH-optimal dynamic programme.
+ * Renders are identical either way; for inspection and the collapse's own tests (ABI 7). */
+#define VR_SCENE_GREEDY_COLLAPSE 16u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split
@@ -242,10 +246,14 @@ int vr_partial_render_scene(const vr_scene* scene, vr_tile tile, uint64_t height
  * is read first when params->accumulate is 1 (update_pixel continuation). */
 int vr_render_tile(const vr_scene* scene, const vr_render_params* params, vr_accumulation_buffer* buf);
 
-/* Device-resident form for the multi-GPU path: `state` is a device pointer to
- * tile_width*tile_height records of 8 doubles {sum X, sum Y, sum Z, bias X, bias Y, bias Z,
- * weight, weight_bias} on the scene's device; `stream` is a hipStream_t (NULL = the scene's own
- * stream) and the call only enqueues work (no host synchronisation). */
+/* Device-resident form for the multi-GPU path: `state` is a device pointer to the tile's records
+ * (ABI 7) -- 8 doubles per pixel in two halves, for the n = tile_width*tile_height pixels in
+ * row-major order:
+ *     state[4p .. 4p+3]           = {sum X, sum Y, sum Z, weight}        (colour_sum, weight)
+ *     state[4n + 4p .. 4n + 4p+3] = {bias X, bias Y, bias Z, weight_bias} (Kahan compensations)
+ * The first half is the merge-exact part: records of disjoint sample sets (one per GPU) merge by
+ * adding it, in place, with one collective over 32 B per pixel.  `stream` is a hipStream_t (NULL =
+ * the null stream) and the call only enqueues work (no host synchronisation). */
 typedef struct vr_launch_stats {
     float kernel_ms;          /* HIP-event time of the render kernel launch(es), valid when timed != 0 */
     uint32_t timed;
@@ -266,8 +274,12 @@ typedef struct vr_launch_stats {
 #define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
 /* with VR_LAUNCH_TIMED: record the HIP events but return without waiting (stats: passes only); the
  * times are read later by vr_collect_launch_times, so back-to-back timed frames leave the GPU no
- * idle gap for a host round trip (ABI 6) */
+ * idle gap for a host round trip (ABI 6).  The caller must collect: a stream holds at most 4096
+ * uncollected deferred launches, beyond which the call fails with VR_ERROR_INVALID_ARGUMENT. */
 #define VR_LAUNCH_DEFER_TIMES 4u
+/* skip the camera-frustum culling of 8x8 pixel blocks (every sample traced): the records are the
+ * same bit for bit (tests/test_gpu_cull.py); for tests and A/B measurements (ABI 7) */
+#define VR_LAUNCH_NO_CULL 8u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
@@ -287,10 +299,11 @@ typedef struct vr_launch_times {
     uint32_t reserved;
 } vr_launch_times;
 int vr_collect_launch_times(const vr_scene* scene, void* stream, vr_launch_times* out);
-/* Mean XYZ of host-side state records: colour = colour_sum * (1 / weight)
- * (accumulation_buffer.rs:59).  States of disjoint sample sets (e.g. one per GPU) merge by
- * element-wise addition of the 8-double records (the cross-GPU reduce), which is what
- * AccumulationBuffer::merge_tile's weighted blend (accumulation_buffer.rs:62-85) computes. */
+/* Mean XYZ of host-side state records (the layout of vr_render_tile_device; only the sums half is
+ * read): colour = colour_sum * (1 / weight) (accumulation_buffer.rs:59).  States of disjoint sample
+ * sets (e.g. one per GPU) merge by element-wise addition of the sums half (the cross-GPU reduce),
+ * which is what AccumulationBuffer::merge_tile's weighted blend (accumulation_buffer.rs:62-85)
+ * computes. */
 int vr_resolve_state(const double* state_host, uint64_t pixel_count, double* colour_out);
 /* AccumulationBuffer::merge_tile (accumulation_buffer.rs:62-85, the host side of main.rs:214-216):
  * for every pixel of `tile` (full-image coordinates in `dst`), dst colour = blend(dst colour, dst
@@ -340,8 +353,8 @@ void vr_mesh_free(double* vertices, double* normals);
 /* AccumulationBuffer::to_image_rgb_u8(&ClampingToneMapper) (accumulation_buffer.rs:38-42,
  * image.rs:166-187, colour_xyz.rs:49-84): XYZ -> linear sRGB (the reference's matrix) ->
  * srgb_gamma (its constants 12.98 / 1.005) -> clamp to [0, 1] -> (v * 255) truncated (NaN -> 0).
- * vr_tone_map_device: `state` = device records (8 f64 per pixel, as vr_render_tile_device
- * writes; colour = colour_sum * (1 / weight), 0 where weight is 0), `rgb_out` = device memory
+ * vr_tone_map_device: `state` = device records (as vr_render_tile_device writes them; only the
+ * sums half is read; colour = colour_sum * (1 / weight), 0 where weight is 0), `rgb_out` = device memory
  * (3 bytes per pixel, row-major); enqueued on `stream` (NULL = the null stream) of `device`.
  * vr_tone_map: host XYZ colour buffer (3 f64 per pixel) -> host RGB bytes. */
 int vr_tone_map_device(const double* state, uint64_t pixel_count, uint8_t* rgb_out, int device, void* stream);
@@ -349,6 +362,13 @@ int vr_tone_map(const double* colour_xyz, uint64_t pixel_count, uint8_t* rgb_out
 /* ImageRgbU8::write_png (image.rs:52-66): 8-bit RGB PNG of `height` rows of `width` pixels
  * (row 0 first).  Host only. */
 int vr_write_png(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+
+/* Upper bound on the staging memory one render call may use (16 B per pixel-sample of a launch;
+ * 0 = the default, half of the free HBM).  A call whose tile x spp needs more runs in several
+ * launches that continue update_pixel in sample order (bit-identical records).  For a GPU shared
+ * with other work, and the tests of the pass split.  Not thread-safe against concurrent render
+ * calls on the same scene: set it before rendering (ABI 7). */
+int vr_scene_set_staging_limit(vr_scene* scene, uint64_t bytes);
 
 /* Test hook (no reference counterpart): every hit on scene object `object` takes the singular-
  * shading-basis path (VR_ERROR_SINGULAR_BASIS, where simple_random_integrator.rs:26-31 panics),

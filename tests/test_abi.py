@@ -41,7 +41,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 6
+    assert lib.vr_abi_version() == 7
     assert isinstance(lib.vr_last_error(), bytes)
 
 

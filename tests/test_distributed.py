@@ -18,6 +18,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from vanrijn_amd import distributed as D
+from vanrijn_amd import records as R
 
 H, W, SEED = 20, 24, 17
 
@@ -35,8 +36,7 @@ def _small_scene():
 
 
 def _records(buf):
-    return np.concatenate([buf["colour_sum"], buf["colour_bias"], buf["weight"][..., None],
-                           buf["weight_bias"][..., None]], axis=-1)
+    return R.from_fields(buf["colour_sum"], buf["colour_bias"], buf["weight"], buf["weight_bias"])
 
 
 def _worker(rank, world, port, total_spp, split, steps, out_path):
@@ -57,7 +57,7 @@ def _worker(rank, world, port, total_spp, split, steps, out_path):
     gathered = [None] * world
     dist.all_gather_object(gathered, firsts)
     if rank == 0:
-        np.save(out_path, state.numpy().reshape(H, W, 8))
+        np.save(out_path, state.numpy())
         np.save(out_path + ".firsts.npy", np.array(gathered))
     dist.barrier()
     dist.destroy_process_group()
@@ -80,15 +80,14 @@ def test_sharded_frame_matches_single_process(tmp_path, world, split):
     orc = O.OracleScene(_small_scene().spec())
     single = _records(orc.render_tile(Tile(0, W, 0, H), H, W, union_spp, seed=SEED, first_sample=union_first,
                                       mode=O.MODE_PRUNED))
-    assert np.array_equal(reduced[..., 6], single[..., 6])  # weights: exact sample counts
-    assert (reduced[..., 3:6] == 0).all() and (reduced[..., 7] == 0).all()  # compensations zeroed on rank 0
+    fr, fs = R.fields(reduced, (H, W)), R.fields(single, (H, W))
+    assert np.array_equal(fr["weight"], fs["weight"])  # weights: exact sample counts
+    assert (R.compensations(reduced) == 0).all()  # compensations zeroed on rank 0
     mean_r = D.mean_colour(torch.from_numpy(reduced)).numpy()
     mean_s = D.mean_colour(torch.from_numpy(single)).numpy()
     assert np.abs(mean_r - mean_s).max() < 1e-12
     # an update_pixel continuation on the reduced state == the same continuation of the union
-    buf = {"colour": np.zeros((H, W, 3)), "colour_sum": reduced[..., 0:3].copy(),
-           "colour_bias": reduced[..., 3:6].copy(), "weight": reduced[..., 6].copy(),
-           "weight_bias": reduced[..., 7].copy()}
+    buf = dict(fr, colour=np.zeros((H, W, 3)))
     nxt = union_first + union_spp
     cont = orc.render_tile(Tile(0, W, 0, H), H, W, 2, seed=SEED, first_sample=nxt, mode=O.MODE_PRUNED,
                            accumulate=buf)
@@ -122,25 +121,40 @@ def test_reduce_is_a_no_op_on_one_process():
 
 
 def test_reduce_moves_only_the_sums():
-    """32 B per pixel -- {sum X, sum Y, sum Z, weight} -- not the whole 64-B record."""
+    """32 B per pixel -- {sum X, sum Y, sum Z, weight} -- not the whole 64-B record,
+    and they are the records' first half: one contiguous in-place buffer (no gather / scatter)."""
     state = torch.zeros(H * W * 8, dtype=torch.float64)
     assert D.reduce_bytes(state) == 32 * H * W
-    assert D.SUMS == (0, 1, 2, 6) and sorted(D.SUMS + D.BIAS_COLUMNS) == list(range(8))
+    s = R.sums(state)
+    assert s.is_contiguous() and s.data_ptr() == state.data_ptr() and s.numel() == 4 * H * W
+    assert R.compensations(state).data_ptr() == state.data_ptr() + 32 * H * W
+
+
+def test_records_fields_round_trip():
+    rng = np.random.default_rng(3)
+    f = {"colour_sum": rng.normal(size=(H, W, 3)), "colour_bias": rng.normal(size=(H, W, 3)),
+         "weight": rng.normal(size=(H, W)), "weight_bias": rng.normal(size=(H, W))}
+    flat = R.from_fields(**f)
+    assert flat.shape == (8 * H * W,)
+    g = R.fields(flat, (H, W))
+    assert all(np.array_equal(f[k], g[k]) for k in f)
+    assert np.array_equal(R.sums(flat)[:, 3], f["weight"].reshape(-1))
 
 
 def _keep_worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rec = torch.arange(5 * 8, dtype=torch.float64).reshape(5, 8) + 100 * rank
+    rec = torch.arange(5 * 8, dtype=torch.float64) + 100 * rank
     mine = rec.clone()
-    D.reduce_records(rec.view(-1))
+    D.reduce_records(rec)
     if rank == 0:
-        want = sum(torch.arange(5 * 8, dtype=torch.float64).reshape(5, 8) + 100 * r for r in range(world))
-        want[:, 3:6] = 0.0
-        want[:, 7] = 0.0
+        want = sum(torch.arange(5 * 8, dtype=torch.float64) + 100 * r for r in range(world))
+        want[20:] = 0.0  # the compensations half
         assert torch.equal(rec, want)
     else:
-        assert torch.equal(rec, mine)  # a non-destination rank keeps its own records
+        # the collective works in place: a non-destination rank's sums half is the collective's
+        # (gloo uses it as scratch), its compensations are untouched
+        assert torch.equal(rec[20:], mine[20:])
     np.save(f"{out_path}.{rank}.npy", rec.numpy())
     dist.barrier()
     dist.destroy_process_group()

@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 from vanrijn_amd import _native as N
+from vanrijn_amd import records as R
 from vanrijn_amd import scenes
 from vanrijn_amd.render import (Tile, collect_launch_times, partial_render_scene, render_tile, render_tile_device,
                                 stream_check_error)
@@ -137,10 +138,10 @@ def test_clean_scene_streams_check_ok(small_main):
     st = torch.zeros(32 * 32 * 8, dtype=torch.float64, device="cuda")
     render_tile_device(ds, Tile(0, 32, 0, 32), 32, 32, 2, 3, 0, st.data_ptr(), s.cuda_stream)
     stream_check_error(ds, s.cuda_stream)
-    assert float(st.reshape(-1, 8)[:, 6].sum()) == 2 * 32 * 32
+    assert float(R.sums(st)[:, 3].sum()) == 2 * 32 * 32
 
 
-def test_deferred_launch_times(small_main, faulty_scene, monkeypatch):
+def test_deferred_launch_times(small_main, faulty_scene):
     """VR_LAUNCH_DEFER_TIMES (bench.py's timed frames): the launches queue without a host wait and
     vr_collect_launch_times returns their summed event times once; the records equal timed launches'
     bit for bit; device errors of deferred launches are reported by the collection."""
@@ -153,7 +154,6 @@ def test_deferred_launch_times(small_main, faulty_scene, monkeypatch):
     assert collect_launch_times(ds, s.cuda_stream)["launches"] == 0  # nothing deferred yet
     timed = [render_tile_device(ds, t, 64, 64, 4, 9, 4 * k, a.data_ptr(), s.cuda_stream, accumulate=k > 0,
                                 timed=True) for k in range(3)]
-    monkeypatch.setenv("VR_STAGING_CAP_MB", "1")  # 64^2 x 4 spp x 16 B = 256 KB: still one pass
     for k in range(3):
         st = render_tile_device(ds, t, 64, 64, 4, 9, 4 * k, b.data_ptr(), s.cuda_stream, accumulate=k > 0,
                                 defer_times=True)

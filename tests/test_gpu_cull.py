@@ -3,7 +3,7 @@
 block_cull_kernel (vr_render.hip) marks the blocks of a launch's tile whose camera rays all miss
 every object by a wide margin; the render kernel skips their work items and the ordered reduce
 applies their samples as the missed camera ray's photon {0, 0} (camera.rs:110-113) without staged
-data.  The records must equal a render with the test off (VR_BLOCK_CULL=0), on a full frame, on a
+data.  The records must equal a render with the test off (VR_LAUNCH_NO_CULL), on a full frame, on a
 tile whose edges cut 8x8 blocks, and for an accumulating continuation (non-zero Kahan
 compensations, accumulation_buffer.rs:44-60).
 """
@@ -24,7 +24,7 @@ def device_scenes():
 @pytest.mark.parametrize("which,tile,hw", [("main", (0, 512, 0, 512), (512, 512)),
                                            ("bench", (37, 333, 11, 250), (300, 400)),
                                            ("main", (5, 203, 100, 300), (300, 400))])
-def test_cull_is_bit_identical(which, tile, hw, device_scenes, monkeypatch):
+def test_cull_is_bit_identical(which, tile, hw, device_scenes):
     ds = device_scenes[which]
     t = Tile(*tile)
     H, W = hw
@@ -34,15 +34,14 @@ def test_cull_is_bit_identical(which, tile, hw, device_scenes, monkeypatch):
     def run(cull):
         # first, other photons into the call contexts' staging buffers (every sample traced, another
         # seed): a sample the render skips but the reduce then reads would show up as a difference
-        monkeypatch.setenv("VR_BLOCK_CULL", "0")
         junk = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
         for k in range(2):
-            render_tile_device(ds, t, H, W, 4, 0x1234 + k, 0, junk.data_ptr(), stream)
-        monkeypatch.setenv("VR_BLOCK_CULL", "1" if cull else "0")
+            render_tile_device(ds, t, H, W, 4, 0x1234 + k, 0, junk.data_ptr(), stream, cull=False)
         st = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
-        render_tile_device(ds, t, H, W, 4, 0x77, 0, st.data_ptr(), stream)
-        render_tile_device(ds, t, H, W, 3, 0x77, 4, st.data_ptr(), stream, accumulate=True)
-        c = render_tile_device(ds, t, H, W, 2, 0x77, 7, st.data_ptr(), stream, accumulate=True, counters=True)
+        render_tile_device(ds, t, H, W, 4, 0x77, 0, st.data_ptr(), stream, cull=cull)
+        render_tile_device(ds, t, H, W, 3, 0x77, 4, st.data_ptr(), stream, accumulate=True, cull=cull)
+        c = render_tile_device(ds, t, H, W, 2, 0x77, 7, st.data_ptr(), stream, accumulate=True, counters=True,
+                               cull=cull)
         torch.cuda.synchronize()
         return st.cpu(), c
 

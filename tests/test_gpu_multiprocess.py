@@ -19,6 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from vanrijn_amd import distributed as D
+from vanrijn_amd import records as R
 
 pytestmark = pytest.mark.gpu
 
@@ -58,7 +59,7 @@ def _worker(rank, world, port, total_spp, split, out_path):
     firsts = [None] * world
     dist.all_gather_object(firsts, first)
     if rank == 0:
-        np.save(out_path, host.numpy().reshape(H, W, 8))
+        np.save(out_path, host.numpy())
         np.save(out_path + ".firsts.npy", np.array(firsts))
     dist.barrier()
     dist.destroy_process_group()
@@ -86,11 +87,12 @@ def test_two_processes_reduce_like_one_render(tmp_path, split):
     dev = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
     render_tile_device(ds, Tile(0, W, 0, H), H, W, world * spp, SEED, firsts[0], dev.data_ptr(),
                        torch.cuda.current_stream().cuda_stream, timed=True)
-    single = dev.cpu().numpy().reshape(H, W, 8)
-    assert np.array_equal(reduced[..., 6], single[..., 6])
-    assert np.array_equal(reduced[..., 6], np.full((H, W), float(world * spp)))
-    assert (reduced[..., 3:6] == 0).all() and (reduced[..., 7] == 0).all()
+    single = dev.cpu().numpy()
+    fr, fs = R.fields(reduced), R.fields(single)
+    assert np.array_equal(fr["weight"], fs["weight"])
+    assert np.array_equal(fr["weight"], np.full(H * W, float(world * spp)))
+    assert (R.compensations(reduced) == 0).all()
     mr = D.mean_colour(torch.from_numpy(reduced)).numpy()
     ms = D.mean_colour(torch.from_numpy(single)).numpy()
     assert np.abs(mr - ms).max() <= 1e-12 * max(1.0, float(np.abs(ms).max()))
-    assert (reduced[..., 0:3] != 0).any()
+    assert (fr["colour_sum"] != 0).any()

@@ -148,19 +148,24 @@ def test_one_sample_fresh_buffer_fast_path(main_pair):
     assert np.array_equal(fast.weight_buffer, np.ones((H, W)))
 
 
-def test_staging_pass_split_is_one_launch(main_pair, monkeypatch):
+def test_staging_pass_split_is_one_launch(main_pair):
     """A frame whose staging exceeds the per-launch cap runs in passes that continue update_pixel in
-    sample order: the records equal one launch bit for bit (VR_STAGING_CAP_MB forces 16 passes)."""
+    sample order: the records equal one launch bit for bit (vr_scene_set_staging_limit forces 16
+    passes)."""
     import torch
-    from vanrijn_amd.render import render_tile_device
+    from vanrijn_amd.render import _scene_handle, render_tile_device
     scene, _ = main_pair
+    ds = _scene_handle(scene, 0)
     H, W, spp = 256, 256, 16
     t = Tile(0, W, 0, H)
     one = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
-    st1 = render_tile_device(scene, t, H, W, spp, 9, 0, one.data_ptr(), timed=True)
-    monkeypatch.setenv("VR_STAGING_CAP_MB", "1")  # 1 MiB = one sample of 65536 pixels per pass
+    st1 = render_tile_device(ds, t, H, W, spp, 9, 0, one.data_ptr(), timed=True)
     split = torch.zeros_like(one)
-    st2 = render_tile_device(scene, t, H, W, spp, 9, 0, split.data_ptr(), timed=True)
+    ds.set_staging_limit(1 << 20)  # 1 MiB = one sample of 65536 pixels per pass
+    try:
+        st2 = render_tile_device(ds, t, H, W, spp, 9, 0, split.data_ptr(), timed=True)
+    finally:
+        ds.set_staging_limit(0)
     assert st1["passes"] == 1 and st2["passes"] == spp
     assert torch.equal(one, split)
 

@@ -109,7 +109,7 @@ def test_device_tone_map_matches_oracle(oracle, tmp_path):
     rgb = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
     tone_map_device(state.data_ptr(), H * W, rgb.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    colour = resolve_state(state.cpu().numpy().reshape(H, W, 8))
+    colour = resolve_state(state.cpu().numpy()).reshape(H, W, 3)
     want = oracle.tone_map(colour)
     got = rgb.cpu().numpy().reshape(H, W, 3)
     assert np.array_equal(got, want)

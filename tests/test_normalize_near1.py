@@ -43,23 +43,6 @@ def test_normalised_vectors_land_in_the_range():
     assert np.array_equal(got, want)
 
 
-def half_recip_near1(b):
-    """vr_device.h half_recip_near1: b = bits(a) - bits(1.0) -> bits of 1.0 / (2.0 * a)."""
-    b = np.asarray(b, dtype=np.int64)
-    r = np.where(b >= 0, ONE - 2 * b, ONE + ((1 - b) >> 1))
-    return 0.5 * r.view(np.float64)
-
-
-def test_sphere_half_reciprocal_bitwise():
-    """Sphere::intersect's one_over_2_a = 1.0 / (2.0 * a) (sphere.rs:65), a = d.d of a normalised
-    direction: every a the kernel's range admits (and 16x more) against IEEE division."""
-    b = np.arange(-65536, 65537, dtype=np.int64)
-    a = (ONE + b).view(np.float64)
-    want = 1.0 / (2.0 * a)
-    got = half_recip_near1(b)
-    assert np.array_equal(got.view(np.int64), want.view(np.int64)), b[got != want][:8]
-
-
 def test_sphere_a_of_normalised_directions_lands_in_the_range():
     """a = ((0 + dx dx) + dy dy) + dz dz (sphere.rs:43-47, fold from 0.0) of the kernel's ray
     directions (normalize / normalize_n1 of arbitrary vectors) lies within a few spacings of 1."""

@@ -1,5 +1,7 @@
 """Per-section wave clock cycles of the render kernel's counting variant (diagnostic).
-    python tools/cycles.py [spp] [scene]"""
+    python tools/cycles.py [spp] [scene]
+Needs a tuning build (VR_COUNTERS_PATH is read only with -DVR_TUNING_VARIANTS: `bash
+tools/build_variant.sh tune -DVR_TUNING_VARIANTS`, then VR_LIBRARY=ab/libtune.so)."""
 import json
 import os
 import sys

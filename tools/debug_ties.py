@@ -43,13 +43,16 @@ print("sah vs device intensity differ:", len(dd), dd[:5])
 for (y, x, k) in dd[:3]:
     print((y, x, k), a["intensity"][y, x, k], b["intensity"][y, x, k], ref["intensity"][y, x, k], a["bounces"][y, x, k])
 # accumulation through render_tile_device
+from vanrijn_amd import records as R  # noqa: E402
 from vanrijn_amd.render import render_tile_device
 outs = {}
 for name, kw in (("sah", {}), ("device", {"device_bvh": True})):
     ds = sc.device_scene(0, **kw)
     st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
     render_tile_device(ds, t, H, W, 3, 0x5EED0001, 0, st.data_ptr())
-    outs[name] = st.cpu().numpy().reshape(H, W, 8)
+    f = R.fields(st)  # per pixel: colour_sum, colour_bias, weight, weight_bias side by side
+    outs[name] = np.concatenate([f["colour_sum"], f["colour_bias"], f["weight"][:, None],
+                                 f["weight_bias"][:, None]], axis=1).reshape(H, W, 8)
 dz = np.argwhere(outs["sah"] != outs["device"])
 print("records differ at", len(dz), dz[:6])
 for (y, x, c) in dz[:4]:

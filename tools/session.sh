@@ -49,6 +49,15 @@ for s in $STEPS; do
           --master-port 29517 bench.py --config $cfg --gpus 1 --steps 2 --warmup 1 --no-cpu-baseline --no-drop-in \
           > gpurun_out/${TAG}_dist_$cfg.json 2> gpurun_out/${TAG}_dist_$cfg.err
       rc=$?; echo "dist $cfg rc=$rc"; cut -c 1-300 gpurun_out/${TAG}_dist_$cfg.json; tail -3 gpurun_out/${TAG}_dist_$cfg.err ;;
+    libtests)
+      # the GPU tests against another build of the library (abx/lib$cfg.so, e.g. the VR_STAGE_GUARD build)
+      VR_LIBRARY=abx/lib$cfg.so timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 \
+          --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_gpu_tests_$cfg.log 2>&1
+      rc=$?; echo "gpu tests ($cfg) rc=$rc"; tail -4 gpurun_out/${TAG}_gpu_tests_$cfg.log ;;
+    culldebug)
+      # tools/debug_cull_pf.py (cut tile, culled vs unculled, staging pre-filled) with abx/lib$cfg.so
+      VR_LIBRARY=abx/lib$cfg.so timeout -k 10 300 python -u tools/debug_cull_pf.py > gpurun_out/${TAG}_culldebug_$cfg.log 2>&1
+      rc=$?; echo "culldebug ($cfg) rc=$rc"; grep -E "differing|guard|->" gpurun_out/${TAG}_culldebug_$cfg.log | head -12 ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1; rc=$?; echo "list rc=$rc" ;;
     *) echo "unknown step $s"; rc=2 ;;

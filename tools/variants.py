@@ -2,6 +2,9 @@
 
     python tools/variants.py --spp 32 --reps 3 --variants 0,1,2,3,4 --thresholds 32
 Prints one JSON line per (variant, threshold) with the median kernel ms over reps.
+The variant / threshold / --env overrides are read only by a tuning build of the library
+(-DVR_TUNING_VARIANTS: `VR_TUNING=1 python -m vanrijn_amd.build`, or `bash tools/build_variant.sh
+NAME -DVR_TUNING_VARIANTS` and VR_LIBRARY=ab/libNAME.so); a default build ignores them.
 """
 import argparse
 import json

@@ -23,7 +23,8 @@ SCENE_HOST_ONLY = 1
 SCENE_DEVICE_BVH = 2
 SCENE_REFERENCE_BVH = 4
 SCENE_DEVICE_SAH = 8
-LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES = 1, 2, 4
+SCENE_GREEDY_COLLAPSE = 16
+LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES, LAUNCH_NO_CULL = 1, 2, 4, 8
 SCENE_INFO_NAN_FREE = 1
 
 
@@ -158,6 +159,7 @@ SIGNATURES = {
     "vr_tone_map_device": (C.c_int, [_p, _u64, _p, _i32, _p]),
     "vr_tone_map": (C.c_int, [_p, _u64, _p, _i32]),
     "vr_write_png": (C.c_int, [C.c_char_p, _p, _u32, _u32]),
+    "vr_scene_set_staging_limit": (C.c_int, [_p, _u64]),
     "vr_debug_set_fault_object": (C.c_int, [_p, _i32]),
     "vr_device_count": (C.c_int, []),
     "vr_last_error": (C.c_char_p, []),

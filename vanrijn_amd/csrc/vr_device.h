@@ -54,9 +54,6 @@ __device__ __forceinline__ V3 normalize(V3 a) {  // vec3.rs:103-110 (multiply by
 // break the ties the first-order values sit on).  On the bits: b = bits(x) - bits(1.0) is k above
 // 1 and -k below.  Every such x is checked against the correctly rounded 1 / sqrt(x) in
 // tests/test_normalize_near1.py; other lanes take normalize's sqrt and division.
-#ifndef VR_NEAR1
-#define VR_NEAR1 1
-#endif
 // every active lane's b (bits of a.a minus bits of 1.0) within +-4096: one unsigned 64-bit compare
 // into a lane mask (llvm.amdgcn.icmp; a ballot of the two signed tests is lowered to two compares,
 // a v_cndmask and a v_cmp)
@@ -64,7 +61,6 @@ __device__ __forceinline__ bool near1_all(int64_t b) {
     return __builtin_amdgcn_uicmpl((uint64_t)(b + 4096), 8192ull, 34 /* ugt */) == 0;
 }
 __device__ __forceinline__ V3 normalize_n1(V3 a) {
-#if VR_NEAR1
     const double x = dot(a, a);
     const int64_t one = 0x3FF0000000000000ll;
     const int64_t b = __double_as_longlong(x) - one;
@@ -78,9 +74,6 @@ __device__ __forceinline__ V3 normalize_n1(V3 a) {
         inv = 1.0 / sqrt(x);
     }
     return mk(a.x * inv, a.y * inv, a.z * inv);
-#else
-    return normalize(a);
-#endif
 }
 __device__ __forceinline__ bool sgn(double x) { return __double_as_longlong(x) < 0; }
 __device__ __forceinline__ double sel(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
@@ -313,13 +306,7 @@ struct RayPre {
     __device__ __forceinline__ bool behind_ok() const { return (flags & 8) != 0; }
 };
 
-// the shear constants alone (calculate_shear_to_z_axis, triangle.rs:129-131): begin_ray may
-// defer them to the ray's first BVH entry (only triangle tests and triangle shading read them)
-__device__ __forceinline__ void prepare_shear(RayPre& p) {
-    p.sx = -sel(p.d, p.k0()) / p.pdz;
-    p.sy = -sel(p.d, p.k1()) / p.pdz;
-}
-__device__ __forceinline__ RayPre prepare(const Ray& r, bool shear = true) {
+__device__ __forceinline__ RayPre prepare(const Ray& r) {
     RayPre p;
     p.o = r.o;
     p.d = r.d;
@@ -330,10 +317,8 @@ __device__ __forceinline__ RayPre prepare(const Ray& r, bool shear = true) {
     else rot = (r.d.z > r.d.y) ? 0 : 2;
     const int k0 = rot, k1 = rot == 2 ? 0 : rot + 1, k2 = rot == 0 ? 2 : rot - 1;
     double pdx = sel(r.d, k0), pdy = sel(r.d, k1), pdz = sel(r.d, k2);
-    if (shear) {
-        p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
-        p.sy = -pdy / pdz;
-    }
+    p.sx = -pdx / pdz;  // calculate_shear_to_z_axis (triangle.rs:129-131)
+    p.sy = -pdy / pdz;
     p.pdz = pdz;
     const double tiny = 1e-150;
     const bool exact_only = !(fabs(r.d.x) > tiny && fabs(r.d.y) > tiny && fabs(r.d.z) > tiny);
@@ -498,21 +483,6 @@ __device__ __forceinline__ double sphere_a(V3 d) {
     a = a + d.z * d.z;
     return a;
 }
-// 1.0 / (2.0 * a) (sphere.rs:65) for a near 1 (every ray direction here is normalised, so a lies
-// within a few spacings of 1), with the bits of the division: 2a is exact and RN(1 / 2a) =
-// RN(1 / a) / 2.  With u = 2^-52 and b = bits(a) - bits(1.0):
-//   a = 1 + b u (b >= 0):      1 / a = 1 - b u + b^2 u^2 ...   rounds to 1 - 2b (u/2): bits(1.0) - 2b;
-//   a = 1 - k u/2 (k = -b > 0): 1 / a = 1 + k u/2 + k^2 u^2/4 ... rounds to 1 + ceil(k/2) u
-// (the second-order terms are positive and far below half a spacing for |b| <= 4096: they only
-// break the tie an odd k sits on, upward).  Checked against IEEE division for every such a in
-// tests/test_normalize_near1.py; a wave with any other a divides.
-__device__ __forceinline__ double half_recip_near1(double a) {
-    const int64_t one = 0x3FF0000000000000ll;
-    const int64_t b = __double_as_longlong(a) - one;
-    if (near1_all(b))
-        return 0.5 * __longlong_as_double(b >= 0 ? one - 2 * b : one + ((1 - b) >> 1));
-    return 1.0 / (2.0 * a);
-}
 // Sphere::intersect (sphere.rs:39-93), decision part: distance or -1; `a` = sphere_a(p.d) and
 // `one_over_2_a` = 1 / (2a) of the ray, hoisted out of the loop over spheres (the same bits)
 __device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p, double a, double one_over_2_a) {
@@ -539,15 +509,14 @@ __device__ __forceinline__ double sphere_distance(const Prim& s, const RayPre& p
     return distance;
 }
 
-// Conservative f32 pre-test for Sphere::intersect: true only if the LINE passes the sphere so far
-// outside that the reference's f64 discriminant b^2 - 4ac is certainly negative (the call returns
-// None).  In exact arithmetic delta = 4|d|^2 (r^2 - dist^2), dist^2 = |oc|^2 - (oc.d)^2 / |d|^2;
+// Conservative f32 pre-test for Sphere::intersect: the sphere is ruled out ("missed") only if the
+// LINE passes it so far outside that the reference's f64 discriminant b^2 - 4ac is certainly
+// negative (the call returns None).  In exact arithmetic delta = 4|d|^2 (r^2 - dist^2), dist^2 = |oc|^2 - (oc.d)^2 / |d|^2;
 // the f64 evaluation errs by O(1e-16 (|o|^2 + |c|^2 + |oc|^2)) and this f32 estimate of
 // dist^2 - r^2 by < 2e-6 |oc|^2 (|d| = 1 +- 1e-16; conversions, products and sums each 6e-8
 // relative), so the margin 1e-4 |oc|^2 + 1e-12 (|o|^2 + |c|^2) covers both.  NaN: not missed.
-__device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p);
-// lanes (of the active ones) whose sphere_missed32 is false, as one v_cmp: !(lhs > rhs) is
-// "unordered or less-equal"
+// the lanes (of the active ones) for which the pre-test cannot rule the sphere out, as one v_cmp:
+// !(lhs > rhs) is "unordered or less-equal"
 __device__ __forceinline__ uint64_t sphere_maybe32_lanes(const Prim& s, const RayPre& p) {
     const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
     const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
@@ -558,41 +527,6 @@ __device__ __forceinline__ uint64_t sphere_maybe32_lanes(const Prim& s, const Ra
     const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
                      (float)s.vec[2] * (float)s.vec[2];
     return __builtin_amdgcn_fcmpf((oc2 - t * t) - r * r, 1e-4f * oc2 + 1e-12f * (po + pc), 13 /* ule */);
-}
-__device__ __forceinline__ bool sphere_missed32(const Prim& s, const RayPre& p) {
-    const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
-    const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
-    const float t = ox * dx + oy * dy + oz * dz;
-    const float oc2 = ox * ox + oy * oy + oz * oz;
-    const float r = (float)s.scalar;
-    const float po = (float)p.o.x * (float)p.o.x + (float)p.o.y * (float)p.o.y + (float)p.o.z * (float)p.o.z;
-    const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
-                     (float)s.vec[2] * (float)s.vec[2];
-    return (oc2 - t * t) - r * r > 1e-4f * oc2 + 1e-12f * (po + pc);
-}
-// sphere_missed32, or the sphere cannot become the closest hit: it lies wholly behind the origin
-// (both roots negative: distance <= 0, None), or its near root lies beyond `best` (the distance
-// the sphere must beat: dd < best fails, the first of equals is kept).  The exact roots are
-// -t -+ sqrt(r^2 - dist^2) (|d| = 1), so both are < 0 when t > r and the near one exceeds
-// -t - r.  The reference's f64 roots err by at most ~5e-8 sqrt(|o|^2 + |c|^2 + |oc|^2) (its
-// discriminant's rounding under the sqrt) and this f32 t by < 3e-7 |oc|_1: the margin
-// m = 1e-4 |oc|_1 + 1e-6 (|o|_1 + |c|_1 + r) covers both (L1 norms bound L2).  best = +inf: no
-// best yet.  NaN anywhere: not skipped.
-__device__ __forceinline__ bool sphere_skip32(const Prim& s, const RayPre& p, float best) {
-    const float ox = (float)(p.o.x - s.vec[0]), oy = (float)(p.o.y - s.vec[1]), oz = (float)(p.o.z - s.vec[2]);
-    const float dx = (float)p.d.x, dy = (float)p.d.y, dz = (float)p.d.z;
-    const float t = ox * dx + oy * dy + oz * dz;
-    const float oc2 = ox * ox + oy * oy + oz * oz;
-    const float r = (float)s.scalar;
-    const float po = (float)p.o.x * (float)p.o.x + (float)p.o.y * (float)p.o.y + (float)p.o.z * (float)p.o.z;
-    const float pc = (float)s.vec[0] * (float)s.vec[0] + (float)s.vec[1] * (float)s.vec[1] +
-                     (float)s.vec[2] * (float)s.vec[2];
-    if ((oc2 - t * t) - r * r > 1e-4f * oc2 + 1e-12f * (po + pc)) return true;
-    const float m = 1e-4f * (fabsf(ox) + fabsf(oy) + fabsf(oz)) +
-                    1e-6f * (fabsf((float)p.o.x) + fabsf((float)p.o.y) + fabsf((float)p.o.z) +
-                             fabsf((float)s.vec[0]) + fabsf((float)s.vec[1]) + fabsf((float)s.vec[2]) + r);
-    if (t - r > m) return true;                                   // behind the origin
-    return (-t - r) - m > best + 1e-6f * fabsf(best) + 1e-30f;  // beyond the best distance
 }
 
 // Plane::intersect (plane.rs:49-75): t or -1 (t == 0 is a hit).  NaN t (ray inside the plane)
@@ -614,68 +548,6 @@ struct HitInfo {
     int material;
 };
 
-// triangle_distance for the leaf round, with the nine vertex components LOADED in the ray's axis
-// order (rotation r = k0: [r, r + 1, r + 2] mod 3) -- a lane-varying address offset per axis
-// instead of two selects per 32-bit half of every component (36 v_cndmask) -- and the hit point
-// formed in the rotated axes (per component the same operations on the same values), its offset
-// from the origin rotated back before the x, y, z sum of squares: the same bits as
-// triangle_distance.  `rank`: the triangle's reference rank (TriVerts::rank).
-__device__ __forceinline__ double triangle_distance_rot(const TriVerts* t, const RayPre& p, int64_t& rank) {
-    const int k0 = p.k0(), k1 = p.k1(), k2 = p.k2();
-    const double* tv = t->v;
-    double px[3], py[3], pz[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        px[i] = tv[3 * i + k0];
-        py[i] = tv[3 * i + k1];
-        pz[i] = tv[3 * i + k2];
-    }
-    rank = t->rank;
-    const double ox = sel(p.o, k0), oy = sel(p.o, k1), oz = sel(p.o, k2);
-    double tx[3], ty[3], az[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const double ax = px[i] + (-ox), ay = py[i] + (-oy);
-        az[i] = pz[i] + (-oz);
-        tx[i] = ax + p.sx * az[i];
-        ty[i] = ay + p.sy * az[i];
-    }
-    const double e0 = tx[1] * ty[2] - tx[2] * ty[1];
-    const double e1 = tx[2] * ty[0] - tx[0] * ty[2];
-    const double e2 = tx[0] * ty[1] - tx[1] * ty[0];
-    const bool s0 = sgn(e0), s1 = sgn(e1), s2 = sgn(e2);
-    if (!((!s0 && !s1 && !s2) || (s0 && s1 && s2))) return -1.0;
-    const double ea0 = fabs(e0), ea1 = fabs(e1), ea2 = fabs(e2);
-    double s = 0.0;
-    s = s + ea0;
-    s = s + ea1;
-    s = s + ea2;
-    const double inv = 1.0 / s;
-    const double b0 = ea0 * inv, b1 = ea1 * inv, b2 = ea2 * inv;
-    double tz = 0.0;
-    tz = tz + az[0] * b0;
-    tz = tz + az[1] * b1;
-    tz = tz + az[2] * b2;
-    if (sgn(tz) != sgn(p.pdz)) return -1.0;
-    // location, rotated: component j is axis k_j (fold from zero, vertex order as triangle.rs:66-71)
-    double l0 = 0.0, l1 = 0.0, l2 = 0.0;
-    l0 = l0 + px[0] * b0;
-    l1 = l1 + py[0] * b0;
-    l2 = l2 + pz[0] * b0;
-    l0 = l0 + px[1] * b1;
-    l1 = l1 + py[1] * b1;
-    l2 = l2 + pz[1] * b1;
-    l0 = l0 + px[2] * b2;
-    l1 = l1 + py[2] * b2;
-    l2 = l2 + pz[2] * b2;
-    const double d0 = ox - l0, d1 = oy - l1, d2 = oz - l2;  // origin - location, rotated
-    // back to x, y, z: r = 0 (d0, d1, d2), r = 1 (d2, d0, d1), r = 2 (d1, d2, d0)
-    const double dx = k0 == 0 ? d0 : (k0 == 1 ? d2 : d1);
-    const double dy = k0 == 0 ? d1 : (k0 == 1 ? d0 : d2);
-    const double dz = k0 == 0 ? d2 : (k0 == 1 ? d1 : d0);
-    const V3 dv = mk(dx, dy, dz);
-    return sqrt(dot(dv, dv));
-}
 
 // triangle_distance's barycentrics only (the winning triangle's shading, whose hit is known):
 // the same operations up to b0..b2, without tz, the location and the distance's sqrt
@@ -705,9 +577,6 @@ __device__ __forceinline__ void triangle_bary(const TriVerts& t, const RayPre& p
 }
 
 // full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96)
-#ifndef VR_RETRO_DIST
-#define VR_RETRO_DIST 0
-#endif
 // `dist`: the hit's distance from triangle_distance, sqrt((o - loc).(o - loc)) over the same loc
 // bits (triangle_bary repeats its operations), so the retro direction's norm is not recomputed
 __device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, double dist, HitInfo& h) {
@@ -728,11 +597,7 @@ __device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const Ray
     h.normal = n;
     h.cotangent = cot;
     h.tangent = normalize_n1(cross(cot, n));  // cot, n: orthogonal unit vectors
-#if VR_RETRO_DIST
-    h.retro = scl(sub(p.o, loc), 1.0 / dist);  // normalize(o - loc): 1 / sqrt(a.a) with sqrt(a.a) == dist
-#else
     h.retro = normalize(sub(p.o, loc));
-#endif
 }
 
 __device__ void prim_info(const Prim& pr, const RayPre& p, double dist, HitInfo& h) {

@@ -292,9 +292,6 @@ float round_upper(double v) {
     return f;
 }
 
-#ifndef VR_WIDE_DP  // 4-wide collapse: SAH-optimal DP (1) or greedy by largest child area (0)
-#define VR_WIDE_DP 1
-#endif
 
 // The render kernel's 4-wide tree, collapsed from a binary tree (the SAH traversal tree, or the
 // reference's median-split tree): starting from a binary node's two children, the interior child
@@ -317,7 +314,7 @@ struct WideBuilder {
         return dx * dy + dy * dz + dz * dx;
     }
 
-    // SAH-optimal collapse (VR_WIDE_DP): a visit of a wide node costs one node step whatever its
+    // SAH-optimal collapse (the default; VR_SCENE_GREEDY_COLLAPSE builds the greedy one): a visit of a wide node costs one node step whatever its
     // children, and is entered with probability ~ its surface area, so the wide tree minimising
     // sum(SA(wide node)) is chosen by a bottom-up DP over the binary tree (as in Ylitie et al.'s
     // wide-BVH collapse, leaf size 1): F(x) = SA(x) + H(x, 4) is x as a wide node; C(x, k), the best
@@ -540,6 +537,8 @@ struct vr_scene {
     // nodes / tris / normals stay empty; the counts below size the device arrays)
     bool device_bvh = false;
     bool device_sah = false;  // VR_SCENE_DEVICE_SAH: the SAH traversal tree too (vr_build.hip)
+    bool greedy_collapse = false;  // VR_SCENE_GREEDY_COLLAPSE: the 4-wide tree by largest child area
+    uint64_t staging_limit = 0;    // vr_scene_set_staging_limit: bytes of staging per call (0: half the free HBM)
     uint64_t node_count = 0, tri_count = 0;
     struct PendingMesh {
         const double* vertices;
@@ -602,6 +601,13 @@ struct CallCtx {
     size_t pinned_bytes = 0;
     void* mask = nullptr;  // camera-frustum culled 8x8 blocks of the call's tile (1 B each)
     size_t mask_bytes = 0;
+    hipStream_t last_stream = nullptr;  // the stream of the last call's work (enqueue_passes)
+    bool used = false;
+    // debug builds (-DVR_STAGE_GUARD): a generation tag beside every staging slot, and the last
+    // pass generation this context used
+    void* tags = nullptr;
+    size_t tag_bytes = 0;
+    uint32_t gen = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -609,14 +615,27 @@ struct CallCtx {
 // page-locked staging and the caller's memory, and vr_merge_tile.  88 B per pixel of host memory
 // traffic is ~5 ms per 1024^2 frame on one core -- more than the GPU's share of a 1-spp render.
 // ---------------------------------------------------------------------------------------------
-// the CPUs this process may run on (sched affinity), at most 16 (VR_HOST_THREADS overrides)
+// Environment overrides exist in tuning builds only (python -m vanrijn_amd.build with VR_TUNING=1,
+// -DVR_TUNING_VARIANTS: tools/variants.py threshold sweeps, tools/cycles.py diagnostics); a default
+// build reads no VR_* variable, so nothing in a user's environment changes rendering or timing.
+static const char* tuning_env(const char* name) {
+#ifdef VR_TUNING_VARIANTS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// the CPUs this process may run on (sched affinity), at most 16 (VR_HOST_THREADS overrides in
+// tuning builds)
 static unsigned host_threads() {
     static const unsigned n = [] {
         unsigned c = 0;
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof set, &set) == 0) c = (unsigned)CPU_COUNT(&set);
         if (c == 0) c = std::thread::hardware_concurrency();
-        if (const char* e = getenv("VR_HOST_THREADS")) c = (unsigned)atoi(e);
+        if (const char* e = tuning_env("VR_HOST_THREADS")) c = (unsigned)atoi(e);
         return std::max(1u, std::min(c, 16u));
     }();
     return n;
@@ -761,7 +780,7 @@ int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render
 // top of the tree, and visits are roughly proportional to area); the other nodes keep their
 // depth-first order.  Only indices change: the walk, and so every result, is the same.
 int hot_node_budget() {
-    static const int k = getenv("VR_HOT_NODES") ? std::max(0, atoi(getenv("VR_HOT_NODES"))) : vr::kHotNodesDefault;
+    static const int k = tuning_env("VR_HOT_NODES") ? std::max(0, atoi(tuning_env("VR_HOT_NODES"))) : vr::kHotNodesDefault;
     return std::min(k, vr::kHotNodesMax);
 }
 
@@ -830,7 +849,7 @@ int hot_prefix(std::vector<vr::Node4>& n4, std::vector<vr::Bvh>& bvhs, int k) {
 
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
-    // greedy collapse; with VR_WIDE_DP the SAH-optimal one instead wherever its (deeper) stack
+    // greedy collapse; unless VR_SCENE_GREEDY_COLLAPSE, the SAH-optimal one instead wherever its (deeper) stack
     // bound keeps the kernel in the greedy tree's LDS stack class (24 / 32 / 48 entries; a larger
     // class would cost workgroups per CU): a node takes the DP expansion when its DP subtree fits
     auto class_limit = [](int st) { return st + 1 <= 24 ? 23 : (st + 1 <= 32 ? 31 : 47); };
@@ -843,7 +862,7 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     std::vector<vr::Node4> opt;
     std::vector<int32_t> oroot(s->bvhs.size());
     int ostack = 0;
-    if (VR_WIDE_DP && !(getenv("VR_WIDE_DP") && atoi(getenv("VR_WIDE_DP")) == 0)) {
+    if (!s->greedy_collapse) {
         WideBuilder D(nodes, opt, true);
         D.limit = class_limit(G.stack);
         for (size_t i = 0; i < s->bvhs.size(); ++i) {
@@ -857,7 +876,7 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
     for (size_t i = 0; i < s->bvhs.size(); ++i) s->bvhs[i].root4 = use_dp ? oroot[i] : groot[i];
     s->wide_stack = use_dp ? ostack : G.stack;
     s->wide_count = s->nodes4.size();
-    if (getenv("VR_WIDE_STATS")) {  // diagnostic: the collapse's SAH objective, sum SA(wide) / SA(root)
+    if (tuning_env("VR_WIDE_STATS")) {  // diagnostic: the collapse's SAH objective, sum SA(wide) / SA(root)
         double sum = 0.0, root = 0.0;
         for (const auto& w : s->nodes4) {
             float u[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
@@ -1054,20 +1073,23 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.block_mask = nullptr;  // per call (enqueue_passes)
     a.live_blocks = nullptr;
     a.live_count = nullptr;
+    a.stage_tag = nullptr;  // debug builds: per call (enqueue_passes)
+    a.stage_gen = 0;
+    a.pad_gen = 0;
     a.fault_object = s->fault_object;
-    const char* th = getenv("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
+    const char* th = tuning_env("VR_SHADE_THRESHOLD");  // tuning hook (tools/variants.py)
     a.shade_threshold = th ? (uint32_t)atoi(th) : 52u;
-    const char* sm = getenv("VR_SHADE_MIN");  // tuning hook: defer shading below this many hits
+    const char* sm = tuning_env("VR_SHADE_MIN");  // tuning hook: defer shading below this many hits
     a.shade_min = sm ? (uint32_t)std::max(0, atoi(sm)) : 16u;
     a.early_stop = s->nan_free ? 1u : 0u;
-    if (const char* es = getenv("VR_EARLY_STOP")) a.early_stop = atoi(es) != 0 && s->nan_free;  // A/B hook (off only)
-    const char* mm = getenv("VR_MISS_MIN");  // tuning hook: defer finishing misses
+    if (const char* es = tuning_env("VR_EARLY_STOP")) a.early_stop = atoi(es) != 0 && s->nan_free;  // A/B hook (off only)
+    const char* mm = tuning_env("VR_MISS_MIN");  // tuning hook: defer finishing misses
     a.miss_min = mm ? (uint32_t)std::max(0, atoi(mm)) : 8u;
-    const char* ch = getenv("VR_CHUNK");  // tuning hook: samples per work item
+    const char* ch = tuning_env("VR_CHUNK");  // tuning hook: samples per work item
     a.chunk = ch ? (uint32_t)std::max(1, atoi(ch)) : 1u;
-    const char* ts = getenv("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end
+    const char* ts = tuning_env("VR_TAIL_SAMPLES");  // tuning hook: single-sample items at the end
     a.tail_samples = ts ? (uint32_t)std::max(0, atoi(ts)) : 0u;
-    const char* gr = getenv("VR_GRAB");  // tuning hook: items per queue atomic
+    const char* gr = tuning_env("VR_GRAB");  // tuning hook: items per queue atomic
     if (gr) {
         a.grab = (uint32_t)std::max(0, atoi(gr));
     } else {
@@ -1083,17 +1105,13 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         const uint64_t g = items / (waves * 80) / 64 * 64;
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
     }
-    const char* lt = getenv("VR_LEAF_THRESHOLD");  // tuning hooks
+    const char* lt = tuning_env("VR_LEAF_THRESHOLD");  // tuning hooks
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
-    const char* ls = getenv("VR_LEAF_STALL");
+    const char* ls = tuning_env("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
-    // tuning hook (A/B): 0 turns the cooperative tail off in a build compiled with -DVR_COOP=1
-    // (the default build compiles it out: rejected, vr_render.hip)
-    const char* co = getenv("VR_COOP");
-    a.coop = co ? (uint32_t)(atoi(co) != 0) : 1u;
-    const char* lf = getenv("VR_LEAF_FEW");  // tuning hook (0: off)
+    const char* lf = tuning_env("VR_LEAF_FEW");  // tuning hook (0: off)
     a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;
-    const char* pr = getenv("VR_PHASE_A_REPS");  // tuning hook
+    const char* pr = tuning_env("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {
         // same f64 operations as the reference's ImageSampler::new / film_to_world
@@ -1123,6 +1141,8 @@ int read_and_clear_error(int32_t* slot, hipStream_t stream) {
     if (flag) {
         VR_HIP(hipMemsetAsync(slot, 0, sizeof flag, stream));
         VR_HIP(hipStreamSynchronize(stream));
+        if (flag & 8)  // debug builds (VR_STAGE_GUARD)
+            return fail(VR_ERROR_DEVICE, "staging guard: the ordered reduce read a staged photon its pass did not write");
         return fail(VR_ERROR_SINGULAR_BASIS,
                     "Normal, tangent and cotangent don't form a valid basis (det == 0); the reference panics here");
     }
@@ -1166,24 +1186,42 @@ void ctx_free_all(CallCtx* c) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->queue) (void)hipFree(c->queue);
+    if (c->tags) (void)hipFree(c->tags);
     delete c;
 }
 
 // Take a context from the scene's pool (a new one when all are in use).  The caller must hand it
 // back with ctx_release; work it enqueued may still run (its `done` event orders the next user).
-int ctx_acquire(vr_scene* s, CallCtx** out) {
+// `want`: the stream the caller will enqueue on (vr_render_tile_device), or none (the host-buffer
+// entry points, which use the context's own stream).
+int ctx_acquire(vr_scene* s, CallCtx** out, const hipStream_t* want = nullptr) {
     {
-        // a free context whose last call's work has finished on the device (its `done` has
-        // completed) first: one taken while its work is still queued orders the new call after it
-        // (hipStreamWaitEvent), which would serialise an asynchronous caller's frames on two
-        // streams; with none idle, a second context is created rather than waiting (so frame k + 1
-        // renders while frame k's launch drains), beyond two the most recent one is reused
+        // In order of preference:
+        //  1. a free context whose last call's work has finished on the device (its `done` has
+        //     completed);
+        //  2. a free context whose last call was enqueued on the caller's own stream: stream order
+        //     already puts the new call after that work, so the hipStreamWaitEvent on `done` costs
+        //     nothing (bench.py's frames queue back to back on one stream and reuse ONE context --
+        //     a second one would allocate a second frame-sized staging buffer, 68.7 GB at C4 / C5,
+        //     inside the timed region, and its smaller cap could split alternate frames into passes);
+        //  3. with none of those and fewer than two contexts, a new one (frame k + 1 on another
+        //     stream then renders while frame k's launch drains); beyond two the most recent one is
+        //     reused (its `done` orders the new call after it).
         std::lock_guard<std::mutex> g(s->ctx_mutex);
         for (size_t i = s->ctx_free.size(); i-- > 0;) {
             if (hipEventQuery(s->ctx_free[i]->done) == hipSuccess) {
                 *out = s->ctx_free[i];
                 s->ctx_free.erase(s->ctx_free.begin() + (ptrdiff_t)i);
                 return VR_OK;
+            }
+        }
+        if (want) {
+            for (size_t i = s->ctx_free.size(); i-- > 0;) {
+                if (s->ctx_free[i]->used && s->ctx_free[i]->last_stream == *want) {
+                    *out = s->ctx_free[i];
+                    s->ctx_free.erase(s->ctx_free.begin() + (ptrdiff_t)i);
+                    return VR_OK;
+                }
             }
         }
         if (!s->ctx_free.empty() && s->ctx_all.size() >= 2) {
@@ -1316,6 +1354,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     if (!s) return fail(VR_ERROR_OUT_OF_MEMORY, "scene allocation failed");
     s->device = device;
     s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
+    s->greedy_collapse = (flags & VR_SCENE_GREEDY_COLLAPSE) != 0;
     s->camera[0] = desc->camera_location.x;
     s->camera[1] = desc->camera_location.y;
     s->camera[2] = desc->camera_location.z;
@@ -1624,6 +1663,12 @@ int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     return VR_OK;
 }
 
+int vr_scene_set_staging_limit(vr_scene* s, uint64_t bytes) {
+    if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
+    s->staging_limit = bytes;
+    return VR_OK;
+}
+
 int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
     if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
     s->fault_object = object < 0 ? -1 : object;
@@ -1681,13 +1726,13 @@ struct DoneOnExit {
 // persistent grid: workgroups per CU of the render kernel (3: 3 waves per SIMD); VR_GRID_PER_CU
 // overrides (diagnostic: throughput against occupancy)
 int grid_per_cu() {
-    static const int per_cu = getenv("VR_GRID_PER_CU") ? std::max(1, atoi(getenv("VR_GRID_PER_CU"))) : 3;
+    static const int per_cu = tuning_env("VR_GRID_PER_CU") ? std::max(1, atoi(tuning_env("VR_GRID_PER_CU"))) : 3;
     return per_cu;
 }
 
 int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* state, hipStream_t st, int32_t* err,
                    bool counting, bool recording, void* records, unsigned long long* counters,
-                   unsigned long long* wg_times, PassEvents* timing = nullptr) {
+                   unsigned long long* wg_times, PassEvents* timing = nullptr, bool no_cull = false) {
     const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
     const uint64_t npix = tw * th;
     if (npix == 0 || p->spp == 0) return VR_OK;
@@ -1695,11 +1740,10 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
     VR_HIP(hipMemGetInfo(&free_b, &total_b));
     // staging for a whole frame when half the free HBM holds it (a 288 GB MI355X: C4 / C5's
     // 68.7 GB on one GPU in one launch -- every extra launch adds the tail of the frame's longest
-    // paths, ~7 ms on the C5 mesh); VR_STAGING_CAP_MB lowers the cap (tests of the pass split)
-    const char* cap_mb = getenv("VR_STAGING_CAP_MB");
-    const size_t cap_env = cap_mb ? (size_t)std::max(1LL, atoll(cap_mb)) << 20 : 0;
+    // paths, ~7 ms on the C5 mesh); vr_scene_set_staging_limit lowers the cap (a GPU shared with
+    // other work; the tests of the pass split)
     size_t cap = (free_b + c->staging_bytes) / 2;
-    if (cap_env) cap = std::min(cap, cap_env);
+    if (s->staging_limit) cap = std::min<size_t>(cap, s->staging_limit);
     uint64_t pass = recording ? p->spp : std::min<uint64_t>(p->spp, std::max<uint64_t>(1, cap / (16 * npix)));
     // the kernel decodes work items with 32-bit block indices: (8x8 blocks) x samples < 2^32
     if (((tw + 7) / 8) * ((th + 7) / 8) * pass >= (1ull << 32))
@@ -1707,11 +1751,20 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
     // the context's previous user (possibly on another stream) must be done with its buffers
     VR_HIP(hipStreamWaitEvent(st, c->done, 0));
     DoneOnExit guard{c->done, st};
+    c->last_stream = st;
+    c->used = true;
     int rc = ctx_grow(&c->staging, &c->staging_bytes, (size_t)(16 * npix * pass), c->done);
     if (rc) return rc;
-    // blocks whose camera rays all miss every object (one small kernel per call; VR_BLOCK_CULL=0
-    // turns the test off)
-    const bool cull = !(getenv("VR_BLOCK_CULL") && atoi(getenv("VR_BLOCK_CULL")) == 0);
+#ifdef VR_STAGE_GUARD
+    if (c->tag_bytes < (size_t)(4 * npix * pass)) {
+        rc = ctx_grow(&c->tags, &c->tag_bytes, (size_t)(4 * npix * pass), c->done);
+        if (rc) return rc;
+        VR_HIP(hipMemsetAsync(c->tags, 0, c->tag_bytes, st));  // generation 0: never written
+    }
+#endif
+    // blocks whose camera rays all miss every object (one small kernel per call; VR_LAUNCH_NO_CULL
+    // turns the test off: the records are the same bit for bit, tests/test_gpu_cull.py)
+    const bool cull = !no_cull;
     const uint8_t* mask = nullptr;
     const uint32_t *live = nullptr, *live_count = nullptr;
     if (cull && !recording) {  // (the record variant writes every sample's record)
@@ -1737,6 +1790,11 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         q.accumulate = (done > 0 || p->accumulate) ? 1u : 0u;
         vr::RenderArgs a = make_args(s, &q, state);
         a.staging = (double*)c->staging;
+#ifdef VR_STAGE_GUARD
+        a.stage_tag = (uint32_t*)c->tags;
+        if (++c->gen == 0) c->gen = 1;
+        a.stage_gen = c->gen;
+#endif
         a.queue = c->queue;
         a.error_flag = err;
         a.block_mask = mask;
@@ -1796,9 +1854,16 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     int32_t* slot = nullptr;
     rc = stream_slot(ms, stream, &slot);
     if (rc) return rc;
+    if (defer) {  // a caller that defers must collect: the pending events are bounded per stream
+        std::lock_guard<std::mutex> g(ms->slot_mutex);
+        auto it = ms->deferred.find(stream);
+        if (it != ms->deferred.end() && it->second.passes.size() >= vr::kMaxDeferredLaunches)
+            return fail(VR_ERROR_INVALID_ARGUMENT,
+                        "too many VR_LAUNCH_DEFER_TIMES launches on this stream without vr_collect_launch_times");
+    }
     std::unique_lock<std::mutex> lock(ms->counter_mutex, std::defer_lock);
     // diagnostic (tools): with counters, VR_WG_TIMES_PATH receives per-workgroup start/end stamps
-    const char* wg_path = counting ? getenv("VR_WG_TIMES_PATH") : nullptr;
+    const char* wg_path = counting ? tuning_env("VR_WG_TIMES_PATH") : nullptr;
     CallScratch wg;
     const uint64_t blocks = (uint64_t)std::max(1, s->cu_count) * grid_per_cu();  // persistent grid limit
     unsigned long long* counters = nullptr;
@@ -1811,10 +1876,10 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     PassEvents pe;
     {
         CtxLease L(ms);
-        rc = ctx_acquire(ms, &L.c);
+        rc = ctx_acquire(ms, &L.c, &st);
         if (rc) return rc;
         rc = enqueue_passes(ms, L.c, p, state, st, slot, counting, false, nullptr, counters,
-                            (unsigned long long*)wg.ptr, timed ? &pe : nullptr);
+                            (unsigned long long*)wg.ptr, timed ? &pe : nullptr, (launch_flags & VR_LAUNCH_NO_CULL) != 0);
         if (rc) return rc;
     }
     if (!timed) return VR_OK;  // errors of this launch: vr_stream_check_error(scene, stream)
@@ -1849,7 +1914,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
     if (counting) {
         unsigned long long c[vr::kCntCount];
         VR_HIP(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
-        if (const char* cp = getenv("VR_COUNTERS_PATH")) {  // diagnostic: the raw counter array
+        if (const char* cp = tuning_env("VR_COUNTERS_PATH")) {  // diagnostic: the raw counter array
             if (FILE* f = std::fopen(cp, "wb")) {
                 std::fwrite(c, sizeof c, 1, f);
                 std::fclose(f);
@@ -1981,7 +2046,7 @@ int vr_render_tile(const vr_scene* s, const vr_render_params* p, vr_accumulation
     volatile int32_t* flag = (volatile int32_t*)((char*)host + payload);  // the error word rides along
     VR_HIP(hipMemcpyAsync((void*)flag, c->error, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     VR_HIP(hipEventRecord(c->done, st));
-    static const bool host_timing = getenv("VR_HOST_TIMING") != nullptr;  // diagnostic (tools/dropin.py)
+    static const bool host_timing = tuning_env("VR_HOST_TIMING") != nullptr;  // diagnostic (tools/dropin.py)
     const auto t_enq = std::chrono::steady_clock::now();
     VR_HIP(hipEventSynchronize(c->done));
     if (*flag) {
@@ -2136,10 +2201,10 @@ int vr_merge_tile(vr_accumulation_buffer* dst, vr_tile t, const vr_accumulation_
 
 int vr_resolve_state(const double* state, uint64_t pixel_count, double* colour) {
     if (!state || !colour) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
-    for (uint64_t i = 0; i < pixel_count; ++i) {
-        const double w = state[8 * i + 6];
+    for (uint64_t i = 0; i < pixel_count; ++i) {  // the sums half of the records (vr_layout.h)
+        const double w = state[4 * i + 3];
         const double inv = 1.0 / w;
-        for (int k = 0; k < 3; ++k) colour[3 * i + k] = w != 0.0 ? state[8 * i + k] * inv : 0.0;
+        for (int k = 0; k < 3; ++k) colour[3 * i + k] = w != 0.0 ? state[4 * i + k] * inv : 0.0;
     }
     return VR_OK;
 }

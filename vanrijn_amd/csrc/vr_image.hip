@@ -39,16 +39,17 @@ __device__ __forceinline__ double dot_m0(double a, double b, double c, double x,
     return s;
 }
 
-// `records` = 8 f64 per pixel (render state: colour = colour_sum * (1 / weight), 0 where no
-// sample landed, as AccumulationBuffer::new leaves it) or 3 f64 per pixel (the colour buffer)
+// `src` = device records (vr_layout.h: npix x {sum X, Y, Z, weight}, then the compensations;
+// colour = colour_sum * (1 / weight), 0 where no sample landed, as AccumulationBuffer::new leaves
+// it) or 3 f64 per pixel (the colour buffer)
 __global__ __launch_bounds__(256) void tonemap_kernel(const double* src, int from_state, uint64_t npix,
                                                       uint8_t* rgb) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
     double x, y, z;
     if (from_state) {
-        const double* r = src + 8 * p;
-        const double w = r[6];
+        const double* r = src + 4 * p;
+        const double w = r[3];
         const double inv = 1.0 / w;
         x = w != 0.0 ? r[0] * inv : 0.0;
         y = w != 0.0 ? r[1] * inv : 0.0;
@@ -71,22 +72,23 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const double* src, int fro
 
 namespace dev {
 // Host AccumulationBuffer layout (accumulation_buffer.rs:6-12, include/vanrijn_amd.h) <-> the
-// device records (8 f64 per pixel).  planar = [colour 3n | colour_sum 3n | colour_bias 3n |
+// device records (vr_layout.h: sums {X, Y, Z, weight} of every pixel, then their compensations).  planar = [colour 3n | colour_sum 3n | colour_bias 3n |
 // weight n | weight_bias n] doubles, so one host array is one contiguous copy.
 __global__ __launch_bounds__(256) void export_buffer_kernel(const double* __restrict__ state, uint64_t npix,
                                                             double* __restrict__ planar) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
-    const double* r = state + p * 8;
-    const double w = r[6];
+    const double* r = state + p * 4;
+    const double* b = state + 4 * npix + p * 4;
+    const double w = r[3];
     const double inv = 1.0 / w;  // accumulation_buffer.rs:59: colour = sum * (1 / weight)
     for (int k = 0; k < 3; ++k) {
         planar[3 * p + k] = w != 0.0 ? r[k] * inv : 0.0;
         planar[3 * npix + 3 * p + k] = r[k];
-        planar[6 * npix + 3 * p + k] = r[3 + k];
+        planar[6 * npix + 3 * p + k] = b[k];
     }
     planar[9 * npix + p] = w;
-    planar[10 * npix + p] = r[7];
+    planar[10 * npix + p] = b[3];
 }
 // A fresh buffer after exactly one sample per pixel (vr_partial_render_scene): weight 1, weight
 // bias 0, and colour / colour_bias follow from colour_sum alone, so only the sums cross PCIe
@@ -95,20 +97,21 @@ __global__ __launch_bounds__(256) void export_sums_kernel(const double* __restri
                                                           double* __restrict__ sums) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
-    const double* r = state + p * 8;
+    const double* r = state + p * 4;
     for (int k = 0; k < 3; ++k) sums[3 * p + k] = r[k];
 }
 __global__ __launch_bounds__(256) void import_buffer_kernel(const double* __restrict__ planar, uint64_t npix,
                                                             double* __restrict__ state) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
-    double* r = state + p * 8;
+    double* r = state + p * 4;
+    double* b = state + 4 * npix + p * 4;
     for (int k = 0; k < 3; ++k) {
         r[k] = planar[3 * npix + 3 * p + k];
-        r[3 + k] = planar[6 * npix + 3 * p + k];
+        b[k] = planar[6 * npix + 3 * p + k];
     }
-    r[6] = planar[9 * npix + p];
-    r[7] = planar[10 * npix + p];
+    r[3] = planar[9 * npix + p];
+    b[3] = planar[10 * npix + p];
 }
 }  // namespace dev
 

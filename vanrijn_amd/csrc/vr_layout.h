@@ -12,6 +12,8 @@ namespace vr {
 constexpr int kRecursionLimit = 128;       // camera.rs:69
 constexpr int kMaxSpectrumSamples = 64;
 constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
+// VR_LAUNCH_DEFER_TIMES launches a stream may hold before vr_collect_launch_times (3 HIP events each)
+constexpr uint32_t kMaxDeferredLaunches = 4096;
 // LDS copy of the top of the 4-wide tree (DeviceScene::hot_count nodes, at most kHotNodesMax:
 // 4 KB of the render kernel's LDS per workgroup at 32); VR_HOT_NODES at scene creation lowers the
 // count.  Measured and rejected: off unless built with -DVR_HOT_MAX=16 / 32
@@ -156,7 +158,7 @@ struct RenderArgs {
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     uint32_t leaf_few;            // ... or at most this many lanes are still traversing
-    uint32_t coop;                // 1: a wave's last path walks its tree with all lanes (the launch's tail)
+    uint32_t pad_args;
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
@@ -172,7 +174,9 @@ struct RenderArgs {
     double rcp_blocks, rcp_bw;
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
     double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
-    double* state;                // [tile pixels][8]
+    // [tile pixels][4] sums {X, Y, Z, weight}, then [tile pixels][4] compensations {X, Y, Z,
+    // weight} (include/vanrijn_amd.h, ABI 7): the cross-GPU reduce adds the first half in place
+    double* state;
     void* records;             // vr_sample_record* (record variant) or nullptr
     unsigned long long* counters;  // [kCntCount] (counting variant) or nullptr
     unsigned long long* wg_times;  // counting variant: [blocks][2] s_memrealtime at start / end, or nullptr
@@ -185,6 +189,11 @@ struct RenderArgs {
     // nullptr: every block of the tile is live
     const uint32_t* live_blocks;
     const uint32_t* live_count;
+    // debug builds only (-DVR_STAGE_GUARD, DESIGN.md section 8 "staging invariant"): beside every
+    // staged photon the launch's generation, which the ordered reduce checks before reading it
+    uint32_t* stage_tag;  // [pass sample][tile pixel], or nullptr
+    uint32_t stage_gen;   // this pass's generation (never 0)
+    uint32_t pad_gen;
 };
 
 struct TraceArgs {
@@ -219,13 +228,13 @@ enum Counter : int {
 // Launch wrappers implemented in vr_render.hip (host-callable).
 int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
                   int grid_limit, void* stream, void* mid_event = nullptr);
-// vr_image.hip: records (from_state = 1, 8 f64 per pixel) or XYZ colour (3 f64) -> sRGB8
+// vr_image.hip: records (from_state = 1, RenderArgs::state's layout) or XYZ colour (3 f64) -> sRGB8
 // the camera-frustum test of every 8x8 block of a launch's tile into mask (RenderArgs::block_mask)
 int launch_block_cull(const RenderArgs& args, uint8_t* mask, void* stream);
 // the live (unculled) blocks of `mask` (n blocks) in order into live[], their number into *count
 int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32_t* count, void* stream);
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
-// vr_image.hip: device records (8 f64 per pixel) <-> the host AccumulationBuffer's five arrays laid
+// vr_image.hip: device records (RenderArgs::state's layout) <-> the host AccumulationBuffer's five arrays laid
 // out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read;
 // 2: records -> colour_sum only, 3 f64 per pixel)
 int launch_buffer_convert(const double* src, double* dst, uint64_t npix, int to_planar, void* stream);

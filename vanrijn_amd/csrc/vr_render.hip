@@ -94,83 +94,34 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
 
 // kRayReady: the lane's next ray (pre.o, pre.d) is set and begin_ray runs once for all such
 // lanes at the end of phase A (one inlined copy for bounce and camera rays alike)
-#ifndef VR_PEND
-#define VR_PEND 8
-#endif
-constexpr int kPend = VR_PEND;  // pending leaf triangles per lane (LDS)
-// Wave-level leaf queue (VR_WAVE_LEAF, default): the leaf triangles a wave's lanes meet go to one
-// FIFO per wave, tagged with the lane whose ray met them, and a leaf round hands the oldest 64 to
-// the 64 lanes -- each tests one against its owner's ray (fetched by cross-lane permute), and the
-// owners merge their results through LDS atomics.  The f64 triangle test then runs with every
-// lane busy; with per-lane queues a round tested one triangle per lane that had one (17 of 64).
+//
+// Wave-level leaf queue: the leaf triangles a wave's lanes meet go to one FIFO per wave, tagged
+// with the lane whose ray met them, and a leaf round hands the oldest 64 to the 64 lanes -- each
+// tests one against its owner's ray (fetched by cross-lane permute), and the owners merge their
+// results through LDS atomics.  The f64 triangle test then runs with every lane busy; with per-lane
+// queues a round tested one triangle per lane that had one (17 of 64).
+//
 // Wave priority by phase (s_setprio; MI355X_MICROARCH.md: VALU issue is arbitrated by priority,
 // then age): a wave stepping BVH nodes or testing leaves -- short, latency-bound bursts ending in
 // a dependent load -- wins issue over waves in long f64 shading sequences, so its next load
 // leaves sooner.  Measured (A/B): traversal 1 / shading 0: main -1.0 %, C5 -2.0 %; the reverse
 // +1.1 %, +3.4 %.
-#ifndef VR_PRIO_A
-#define VR_PRIO_A 0
-#endif
-#ifndef VR_PRIO_NODE
-#define VR_PRIO_NODE 1
-#endif
-#ifndef VR_PRIO_LEAF
-#define VR_PRIO_LEAF 1
-#endif
-#ifndef VR_SPHERE_SKIP  // f32 sphere skip: line miss, behind the origin or beyond the best hit
-#define VR_SPHERE_SKIP 0
-#endif
-#ifndef VR_PLANE_SIGN  // begin_ray: skip the plane division when every lane's plane lies behind it
-#define VR_PLANE_SIGN 0
-#endif
-#ifndef VR_LAZY_SHEAR  // begin_ray: shear constants at the first BVH entry
-#define VR_LAZY_SHEAR 0
-#endif
-#ifndef VR_LATE_BOX  // leaf round: the exact box test only for entries whose triangle hits
-#define VR_LATE_BOX 1
-#endif
-#ifndef VR_ROT_LOAD  // leaf round: vertex components loaded in the owner ray's axis order (A/B: rejected)
-#define VR_ROT_LOAD 0
-#endif
-#ifndef VR_WAVE_LEAF
-#define VR_WAVE_LEAF 1
-#endif
-// begin_ray's sphere test: 1 -- a and 1 / (2a) once per ray (near-unit reciprocal), kept live across
-// the primitive loop: rejected (main +1.0 %, bench +1.6 %, C5 -1.3 %, profiles/r03/ab_hoist_skip.txt);
-// 2 -- per sphere, 1 / (2a) by the near-unit reciprocal instead of the division: rejected too (main
-// +1.6 %, bench and C5 +-0.5 %, profiles/r03/ab_sphere_near1.txt); 0 -- the division (default)
-#ifndef VR_SPHERE_HOIST
-#define VR_SPHERE_HOIST 0
-#endif
-#ifndef VR_LEAF_SKIP  // node step: skip the FIFO append when no lane met a leaf
-#define VR_LEAF_SKIP 1
-#endif
-// the launch's tail: a wave's last path walks its tree with every lane (RenderArgs::coop).  Parity-
-// green and the lone path 1.9x faster (profiles/r03/longpath_coop.jsonl), but rejected: inside the
-// node step main +5 %, C5 +9 % (profiles/r03/ab_coop_in_node_step.txt); as a tail-only call main
-// +1.5 %, C5 +6.7 %, bench scene +2 %, while C1 gains only 2.5 % -- its long paths share waves, so
-// one live lane per wave is rare (profiles/r03/ab_coop.txt, small_frames_coop.jsonl)
-#ifndef VR_COOP
-#define VR_COOP 0
-#endif
-#ifndef VR_WATCHDOG
+//
+// Experiments measured and rejected in rounds 2-3 (the f32 sphere skip, the plane-sign skip, lazy
+// shear constants, per-lane leaf queues, rotated vertex loads, the hoisted sphere reciprocal, the
+// cooperative tail, the partial child sort, plain staging stores) were removed from the source in
+// round 4; their code is kept as a patch (profiles/r04/removed_experiments.patch) and their A/B
+// numbers in DESIGN.md.
+constexpr int kPrioA = 0, kPrioNode = 1, kPrioLeaf = 1;
+#ifndef VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
 #define VR_WATCHDOG 0
 #endif
-#ifndef VR_STAGE_NT  // staged photons written with the non-temporal hint (A/B: plain stores)
-#define VR_STAGE_NT 1
-#endif
+constexpr int kPend = 8;  // FIFO entries per lane of a wave, on average
 constexpr int kWaveList = 64 * kPend;
-// room for a node step's leaves: per lane (at most kPend queued per lane), or -- VR_WAVE_CAP --
-// for the wave (the FIFO has room for a step of all 64 lanes: any one lane may queue more)
-#ifndef VR_WAVE_CAP
-#define VR_WAVE_CAP 1
-#endif
-#if VR_WAVE_LEAF && VR_WAVE_CAP
-#define VR_ROOM (q_tail - q_head <= (uint32_t)(kWaveList - 256))
-#else
-#define VR_ROOM (np <= kPend - 4)
-#endif  // FIFO entries per wave: each lane owns at most kPend
 static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
+// Room for a node step's leaves: the wave FIFO can take a step of all 64 lanes (4 leaves each), so
+// any one lane may queue more than kPend.  Wave-uniform (q_head / q_tail are).
+#define VR_ROOM (q_tail - q_head <= (uint32_t)(kWaveList - 256))
 
 // The kernel argument block, re-read through a pointer the compiler cannot prove unchanged: the
 // tree and triangle base pointers become scalar loads at their use.  Held in SGPRs for the whole
@@ -198,22 +149,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                                                            const Material* __restrict__ g_materials,
                                                            const Bvh* __restrict__ g_bvhs) {
     __shared__ uint32_t st_node[STACK * 256];
-    // leaf triangles met during traversal wait here for a leaf round, in which every lane with
-    // one tests it: the f64 triangle test then runs for many lanes at once instead of for the few
-    // that reached a leaf in this step.  [slot][thread], LIFO, kPend slots per lane.
-#if VR_WAVE_LEAF
-    // per wave: the FIFO of queued leaves (triangle | exact-box flag, and the owning lane) and, per
-    // owner lane, one leaf round's results: entries tested, min distance bits, and (max rank at
-    // that distance, its triangle)
+    // leaf triangles met during traversal wait for a leaf round, in which every lane tests one: the
+    // f64 triangle test then runs for many lanes at once instead of for the few that reached a leaf
+    // in this step.  Per wave: the FIFO of queued leaves (triangle | exact-box flag, and the owning
+    // lane) and, per owner lane, one leaf round's results: entries tested, min distance bits, and
+    // (max rank at that distance, its triangle)
     __shared__ int32_t wl_tri[4 * kWaveList];
     __shared__ uint8_t wl_own[4 * kWaveList];
     __shared__ unsigned long long lr_d[256], lr_key[256];  // key: rank << 32 | triangle
     __shared__ uint32_t lr_cnt[256];
     const int wbase = (threadIdx.x >> 6) * kWaveList;
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
-#else
-    __shared__ int32_t st_pend[kPend * 256];
-#endif
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
 #if VR_HOT_MAX
@@ -225,11 +171,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     for (uint32_t i = tid; i < hot_n * 8; i += 256) hot4[i] = reinterpret_cast<const uint4*>(A.scene.nodes4)[i];
     __syncthreads();
 #endif
-#if VR_WAVE_LEAF
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
     lr_key[tid] = 0;
     lr_cnt[tid] = 0;
-#endif
     DeviceScene S = A.scene;
     S.prims = g_prims;
     S.materials = g_materials;
@@ -329,7 +273,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             set_cull_far();
         }
     };
-#if VR_WAVE_LEAF
     // One leaf round over the n (<= 64) oldest entries of the wave FIFO: lane i tests entry i
     // against its owner's ray.  Per owner, the round's candidate is the minimum distance and, among
     // equal distances, the highest reference rank (LDS atomics; one wave's LDS operations execute
@@ -349,13 +292,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         op.o.x = __shfl(pre.o.x, (int)owner);
         op.o.y = __shfl(pre.o.y, (int)owner);
         op.o.z = __shfl(pre.o.z, (int)owner);
-#if !VR_LATE_BOX
-        if (__ballot(mine && e < 0)) {  // the direction only for the exact box test (slab)
-            op.d.x = __shfl(pre.d.x, (int)owner);
-            op.d.y = __shfl(pre.d.y, (int)owner);
-            op.d.z = __shfl(pre.d.z, (int)owner);
-        }
-#endif
         op.sx = __shfl(pre.sx, (int)owner);
         op.sy = __shfl(pre.sy, (int)owner);
         op.pdz = __shfl(pre.pdz, (int)owner);
@@ -364,22 +300,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         double d = -1.0;
         uint32_t rank = 0;
         const int tri = e & 0x7fffffff;
-#if VR_LATE_BOX
         // The exact box test decides only where the triangle test hits: a leaf whose triangle
         // misses adds nothing whichever way its box test goes (bvh.rs:77-120 tests the triangle only
         // inside a hit box), so the reference's box decision is taken after the triangle test and
         // only for hitting entries -- the wave runs the six f64 divisions only when such an entry
         // exists, not whenever an entry's f32 box test was too close to call.  The counting variant
         // tests every flagged box, so its counters stay the reference's.
-#if VR_ROT_LOAD
-        if (mine) {
-            // vertex components loaded in the owner ray's axis order (no per-component selects)
-            int64_t rk;
-            d = triangle_distance_rot(VR_TRIS + tri, op, rk);  // the owner's shear constants, not its direction
-            rank = (uint32_t)rk;
-            if (COUNT && e >= 0) cnt.tri_tests++;
-        }
-#else
         TriVerts tv;
         if (mine) {
             tv = load_tri(VR_TRIS + tri);
@@ -388,7 +314,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             rank = (uint32_t)tv.rank;
             if (COUNT && e >= 0) cnt.tri_tests++;
         }
-#endif
         // lanes with an entry (lane < n) whose box was too close to call (e < 0) and whose triangle
         // hits (d >= 0), as compares into lane masks
         const uint64_t flagged = __builtin_amdgcn_uicmp(lane, n, 36 /* ult */) & lanes_igt(0, e);
@@ -400,9 +325,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 VR_SEC(2);
                 VR_MARK("exact_box");
                 if (COUNT) cnt.exact_boxes++;
-#if VR_ROT_LOAD
-                const TriVerts tv = load_tri(VR_TRIS + tri);  // in x, y, z order (rare path)
-#endif
                 double bb[6], lo, hi;
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
@@ -415,31 +337,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
         }
         if (mine) atomicAdd(&lr_cnt[oslot], 1u);
-#else
-        if (mine) {
-            const TriVerts tv = load_tri(VR_TRIS + tri);
-            bool reach = true;
-            if (e < 0) {  // the leaf's f32 box test was too close to call: the exact one decides
-                VR_SEC(2);
-                VR_MARK("exact_box");
-                if (COUNT) cnt.exact_boxes++;
-                double bb[6], lo, hi;
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    bb[2 * a] = fmin(fmin(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
-                    bb[2 * a + 1] = fmax(fmax(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
-                }
-                reach = slab(bb, op, lo, hi);
-            }
-            if (reach) {
-                if (COUNT) cnt.tri_tests++;
-                double b[3];
-                d = triangle_distance(tv, op, b);
-                rank = (uint32_t)tv.rank;
-            }
-            atomicAdd(&lr_cnt[oslot], 1u);
-        }
-#endif
         const bool hit = mine && d >= 0.0;
         const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
         if (hit) atomicMin(&lr_d[oslot], bits);
@@ -472,7 +369,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             lr_key[tid] = 0;
         }
     };
-#endif
     // next BVH (from bvh_i) with work; false when the ray is fully traced
     auto start_bvhs = [&]() {
         for (; bvh_i < S.bvh_count; ++bvh_i) {
@@ -489,9 +385,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 double lo, hi;
                 if (!slab(bvh.root_box, pre, lo, hi) || culled(lo, hi)) continue;
             }
-            // the ray meets a BVH: its triangle tests need the shear constants (a ray whose wave
-            // meets no BVH skips the two divisions; set again per BVH entry, the same bits)
-            if (VR_LAZY_SHEAR) prepare_shear(pre);
             if (bvh.root4 < 0) {  // a one-triangle BVH
                 test_tri(~bvh.root4);
                 continue;
@@ -506,63 +399,28 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // there, not in registers of its own that would stay live through the traversal phase):
     // primitive lists first, then the BVHs
     auto begin_ray = [&]() {
-        pre = prepare(Ray{pre.o, pre.d}, !VR_LAZY_SHEAR);  // shear constants: at the first BVH entry
+        pre = prepare(Ray{pre.o, pre.d});
         pre32 = prepare32(pre, S.extent);
         if (COUNT) cnt.rays++;
         best.kind = kNone;
         best.d = 0.0;
         best.index = -1;
         best.object = 0x7fffffff;
-#if VR_SPHERE_HOIST == 1
-        double sa = 0.0, s2a = 0.0;  // the ray's sphere a and 1 / (2a), once per ray
-        bool have_a = false;
-#endif
         for (int i = 0; i < S.prim_count; ++i) {
             const Prim& pr = S.prims[i];
             double dd;
             bool ok;
             if (pr.kind == 0) {
-#if VR_PLANE_SIGN
-                // t = num / dn < 0 whenever num and dn are nonzero with opposite signs (no underflow
-                // to -0 for |num| > 1e-300, |dn| < 1e290): the wave skips the division when that
-                // holds for every lane (bounce rays leaving the plane, upward rays above it)
-                {
-                    const V3 n = ldv(pr.vec);
-                    const double dn = dot(pre.d, n), num = dot(sub(ldv(pr.pre), pre.o), n);
-                    const bool behind = ((num < 0.0 && dn > 0.0) || (num > 0.0 && dn < 0.0)) && fabs(num) > 1e-300 &&
-                                        fabs(dn) < 1e290;
-                    if (__ballot(!behind) == 0) continue;
-                }
-#endif
                 ok = plane_distance(pr, pre, dd);
             } else {
                 // the f64 test is skipped only when, for every lane, the line clearly misses the
                 // sphere or the sphere lies behind the origin or beyond the lane's best distance
                 // (camera rays of a wave are coherent; so are many bounce rays)
-#if VR_SPHERE_SKIP
-                const float bd = best.kind ? (float)best.d : INFINITY;
-                if (__ballot(!sphere_skip32(pr, pre, bd)) == 0) continue;
-#else
                 if (sphere_maybe32_lanes(pr, pre) == 0) continue;
-#endif
-#if VR_SPHERE_HOIST == 2
-                {
-                    const double a1 = sphere_a(pre.d);
-                    dd = sphere_distance(pr, pre, a1, half_recip_near1(a1));
-                }
-#elif VR_SPHERE_HOIST
-                if (!have_a) {  // wave-uniform: the first sphere this ray's wave tests exactly
-                    sa = sphere_a(pre.d);
-                    s2a = half_recip_near1(sa);
-                    have_a = true;
-                }
-                dd = sphere_distance(pr, pre, sa, s2a);
-#else
                 {
                     const double a1 = sphere_a(pre.d);
                     dd = sphere_distance(pr, pre, a1, 1.0 / (2.0 * a1));
                 }
-#endif
                 ok = dd >= 0.0;
             }
             if (ok && (!best.kind || dd < best.d)) {  // min_by keeps the first of equals
@@ -592,12 +450,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
         // streamed once to HBM and read once by the reduce: non-temporal, so the 16 B per sample
         // (4.3 GB per 1024^2 x 256 frame) do not evict the BVH and triangles from L2 and MALL
-#if VR_STAGE_NT
         __builtin_nontemporal_store(wl, &out[0]);
         __builtin_nontemporal_store(I, &out[1]);
-#else
-        out[0] = wl;
-        out[1] = I;
+#ifdef VR_STAGE_GUARD  // debug builds: this slot now holds this pass's photon
+        A.stage_tag[(uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px] = A.stage_gen;
 #endif
         if (RECORD) {
             const double Is = I * 360.0;
@@ -788,116 +644,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         state = kRayReady;
     };
 
-#if VR_COOP && VR_WAVE_LEAF
-    // The launch's tail: the queue is exhausted and one path is left in the wave (a long path --
-    // e.g. 128 mirror bounces in a crease of the reflective bench scene -- makes a small frame's
-    // time).  Its walk is spread over the wave's lanes (VR_COOP): each step takes the current node
-    // and up to 63 entries from the top of the owner's stack, one per lane, tests them against the
-    // owner's ray, pushes the hit interior children back and queues the hit leaves for the owner;
-    // the stack spans every lane's column of the wave (the other lanes are done).  Culling and the
-    // order-independent leaf rounds keep the closest hit and its tie rule:
-    // only the visiting order changes.  Called with the whole wave active, owner wave-uniform; the
-    // main loop's node step pays one scalar branch for it.
-    auto coop_step = [&](const int owner) {
-        uint32_t lmask = 0;
-        int32_t lent[4];
-        const int o_sp = __builtin_amdgcn_readlane(sp, owner);
-        const int o_node = __builtin_amdgcn_readlane(node, owner);
-        const bool o_trav = __builtin_amdgcn_readlane(state == kTraversing ? 1 : 0, owner) != 0;
-        const int have = o_trav ? (o_node >= 0 ? 1 : 0) + o_sp : 0;
-        constexpr int kCap = 64 * STACK;  // the big stack: every lane column of the wave
-        // entries taken this step: at most 64, and at most what keeps 150 entries of
-        // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a
-        // near-full stack needs at most 3 per level below)
-        int t = have < 64 ? have : 64;
-        const int room = (kCap - 150 - have) / 3;
-        if (t > room) t = room < 1 ? (have > 0 ? 1 : 0) : room;
-        if (t > 0 && VR_ROOM) {
-            VR_MARK("coop_step");
-            // virtual stack index v of the owner -> its LDS word: v < STACK is the owner's own
-            // column (the usual layout), then the next lanes' columns in turn
-            auto vaddr = [&](int v) { return (v % STACK) * 256 + (tid & ~63) + ((owner + v / STACK) & 63); };
-            const int first_stack = o_node >= 0 ? 1 : 0;  // lane 0 takes the current node
-            int my = -1;
-            if ((int)lane < t) my = ((int)lane < first_stack) ? o_node : (int)st_node[vaddr(o_sp - 1 - ((int)lane - first_stack))];
-            const int base = o_sp - (t - first_stack);  // stack entries left below the taken ones
-            Ray32 r;  // the owner's ray and cull bounds, wave-uniform
-            r.ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ox), owner));
-            r.oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oy), owner));
-            r.oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.oz), owner));
-            r.ix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ix), owner));
-            r.iy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iy), owner));
-            r.iz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.iz), owner));
-            r.nx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nx), owner));
-            r.ny = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ny), owner));
-            r.nz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.nz), owner));
-            r.ek = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre32.ek), owner));
-            const float cf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_far), owner));
-            const float cb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cull_behind), owner));
-            uint32_t im = 0;  // hit interior children
-            int c[4];
-            if (my >= 0) {
-                const Node4& nd = VR_NODES4[my];
-                if (COUNT) cnt.node_visits++;
-                uint32_t xm = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    c[k] = nd.child[k];
-                    float f, g;
-                    bool maybe, sure;
-                    slab32_flags(nd.box[k], r, f, g, maybe, sure);
-                    const bool lv = c[k] != kEmptyChild;
-                    if (COUNT && lv) cnt.box_tests++;
-                    const bool pass = lv && maybe && !(f > cf || g < cb);
-                    xm |= (pass && !sure) ? 1u << k : 0u;
-                    im |= (pass && c[k] >= 0) ? 1u << k : 0u;
-                    lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
-                    lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
-                }
-            }
-            // interior hits onto the owner's stack, in (child slot, lane) order
-            int pos = base;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool ih = (im >> k) & 1u;
-                const uint64_t m = __ballot(ih);
-                if (ih) st_node[vaddr(pos + (int)lanes_below(m))] = (uint32_t)c[k];
-                pos += (int)__popcll(m);
-            }
-            // the owner's next node: the top of its stack
-            if ((int)lane == owner) {
-                sp = pos;
-                if (sp > 0) {
-                    --sp;
-                    node = (int)st_node[vaddr(sp)];
-                } else {
-                    node = -1;
-                }
-            }
-        }
-        // the hit leaves, queued for the owner in (child slot, lane) order
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool lh = (lmask >> k) & 1u;
-            const uint64_t m = __ballot(lh);
-            if (lh) {
-                const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
-                wl_tri[wbase + pos] = lent[k];
-                wl_own[wbase + pos] = (uint8_t)owner;
-            }
-            q_tail += (uint32_t)__popcll(m);
-            if ((int)lane == owner) np += (int)__popcll(m);
-        }
-        q_tail = __builtin_amdgcn_readfirstlane(q_tail);
-    };
-#endif
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
         // that only meet the plane or spheres), so those lanes do not idle through phase B
         for (int rep = 0; rep < A.phase_a_reps; ++rep) {
             VR_MARK("phaseA_top");
-            __builtin_amdgcn_s_setprio(VR_PRIO_A);
+            __builtin_amdgcn_s_setprio(kPrioA);
             if (COUNT && first_active_lane()) cnt.outer_slots += 64;
             VR_STAMP(5);
             // shading is deferred while fewer than shade_min lanes have a hit to shade and other
@@ -1065,25 +818,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (COUNT && first_active_lane()) cnt.trav_slots += 64;
             VR_STAMP(5);
             VR_MARK("phaseB_top");
-            __builtin_amdgcn_s_setprio(VR_PRIO_NODE);
-            // node step (4-wide node): lanes with room for four more pending leaves
-#if VR_WAVE_LEAF
+            __builtin_amdgcn_s_setprio(kPrioNode);
+            // node step (4-wide node), while the wave FIFO has room for four more leaves per lane
             uint32_t lmask = 0;  // leaf children this lane queues in this step
             int32_t lent[4];
-#endif
-            bool coop = false;
             if (COUNT) {  // how full this iteration's node step is (the headroom of merging waves)
                 const int n = VR_ROOM ? __popcll(lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) : 0;
                 if (first_active_lane()) step_hist[n == 0 ? 0 : 1 + (n - 1) / 8]++;
             }
-#if VR_COOP && VR_WAVE_LEAF
-            if (A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
-                const uint64_t live = __ballot(state != kDone);
-                coop = __popcll(live) == 1;
-                if (coop) coop_step((int)__builtin_ctzll(live));
-            }
-#endif
-            if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
+            if (state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
 #if VR_HOT_MAX
                 // the node's 112 B (boxes, links): from LDS for the hot top of the tree
@@ -1128,21 +871,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     hm |= pass ? 1u << k : 0u;
                     xm |= (pass && !sure) ? 1u << k : 0u;
                 }
-                // leaf children: queue their triangles (per-lane queue: unconditional LDS writes,
-                // the count advances only for hits; np <= kPend - 4 leaves room for all four;
-                // wave queue: appended after the step, by all lanes at once)
+                // leaf children: their triangles go to the wave FIFO, appended after the step by all
+                // lanes at once
                 float key[4];
                 int ch[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const bool h = (hm >> k) & 1u;
-#if VR_WAVE_LEAF
                     lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
                     lmask |= (h && c[k] < 0) ? 1u << k : 0u;
-#else
-                    st_pend[np * 256 + tid] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
-                    np += (h && c[k] < 0) ? 1 : 0;
-#endif
                     // hit: a finite key (NaN or infinite f32 bounds of exactly-decided children
                     // clamp into range); INFINITY marks "not descended"
                     key[k] = (h && c[k] >= 0) ? fminf(fmaxf(f[k], -FLT_MAX), FLT_MAX) : INFINITY;
@@ -1161,10 +898,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 cas(0, 1);
                 cas(2, 3);
                 cas(0, 2);
-#ifndef VR_SORT_LIGHT  // experiment: nearest first, the other three only partly ordered
                 cas(1, 3);
                 cas(1, 2);
-#endif
                 if (key[0] < INFINITY) {
                     // farthest first, so the nearest remaining pops first (writes at sp are
                     // unconditional: the stack holds one spare entry)
@@ -1184,12 +919,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             VR_STAMP(3);
             VR_MARK("leaf_check");
-            __builtin_amdgcn_s_setprio(VR_PRIO_LEAF);
-#if VR_WAVE_LEAF
-            // append this step's leaves to the wave FIFO in (child slot, lane) order
-#if VR_LEAF_SKIP
+            __builtin_amdgcn_s_setprio(kPrioLeaf);
+            // append this step's leaves to the wave FIFO in (child slot, lane) order (skipped when no
+            // lane met a leaf: main -1.3 %, C5 -4.5 %)
             if (lanes_ine((int)lmask, 0))
-#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool lh = (lmask >> k) & 1u;
@@ -1215,7 +948,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const bool room = VR_ROOM;  // wave-uniform
                 const uint64_t at_node = trav & lanes_ige(node, 0);
                 const uint64_t stalled_m = lanes_igt(np, 0) & (room ? ~lanes_ige(node, 0) : exec_mask());
-                const bool few = coop || (tail && __popcll(trav) <= (int)A.leaf_few);
+                const bool few = tail && __popcll(trav) <= (int)A.leaf_few;
                 if (queued >= A.leaf_threshold || few || __popcll(stalled_m) >= (int)A.leaf_stall ||
                     !room || at_node == 0) {
                     VR_SEC(0);
@@ -1224,24 +957,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     q_head = __builtin_amdgcn_readfirstlane(q_head + (queued < 64u ? queued : 64u));
                 }
             }
-#else
-            // leaf round: enough lanes have a pending triangle, or enough lanes (or all) are
-            // stalled on theirs
-            const uint64_t pm = __ballot(np > 0);
-            if (pm != 0) {
-                const bool stalled = np > 0 && (node < 0 || np > kPend - 4);
-                const uint64_t stm = __ballot(stalled);
-                if (__popcll(pm) >= (int)A.leaf_threshold || __popcll(stm) >= (int)A.leaf_stall ||
-                    __ballot(state == kTraversing && node >= 0 && np <= kPend - 4) == 0) {
-                    if (np > 0) {
-                        VR_SEC(0);
-                        VR_MARK("leaf_test");
-                        --np;
-                        test_tri(st_pend[np * 256 + tid]);
-                    }
-                }
-            }
-#endif
             VR_STAMP(4);
             if (state == kTraversing && node < 0 && np == 0) {
                 VR_SEC(8);
@@ -1411,20 +1126,40 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 __constant__ double c_exp_tab[64] = VR_EXP_TABLE_INIT;
 __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const double* staging, uint64_t npix,
                                                          uint32_t spp, uint32_t accumulate, const uint8_t* mask,
-                                                         uint64_t tile_width) {
+                                                         uint64_t tile_width, const uint32_t* stage_tag,
+                                                         uint32_t stage_gen, int32_t* error_flag) {
+    // Debug builds (-DVR_STAGE_GUARD): every staged photon the reduce reads must carry this pass's
+    // generation -- a slot the render kernel did not write in this pass is a device error (error
+    // word bit 3, VR_ERROR_DEVICE "staging guard").  The invariant it checks: the reduce reads
+    // slot (s, p) exactly for the pixels p < npix outside culled blocks and the samples s < spp,
+    // and the render kernel's item space covers exactly those (pixel, sample) pairs.
+#ifdef VR_STAGE_GUARD
+    auto guard = [&](uint32_t s, uint64_t p) {
+        if (stage_tag[(uint64_t)s * npix + p] != stage_gen) {
+            if (atomicOr(error_flag, 8) == 0)
+                printf("vr staging guard: pixel %llu sample %u tag %u, pass generation %u\n", (unsigned long long)p, s,
+                       stage_tag[(uint64_t)s * npix + p], stage_gen);
+            atomicOr(error_flag, 8);
+        }
+    };
+#define VR_GUARD(s, p) guard(s, p)
+#else
+#define VR_GUARD(s, p) ((void)stage_tag, (void)stage_gen, (void)error_flag)
+#endif
     __shared__ double etab[64];  // 2^(j/64) for the lobes' exp (vr_exp_table.h)
     if (threadIdx.x < 64) etab[threadIdx.x] = c_exp_tab[threadIdx.x];
     __syncthreads();
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
+    // records (vr_layout.h): the pixel's sums {X, Y, Z, weight} at state[4p], its Kahan
+    // compensations at state[4 npix + 4p] -- 32 B each, one dwordx4 pair per half
+    d2* const rs = reinterpret_cast<d2*>(state + 4 * p);
+    d2* const rb = reinterpret_cast<d2*>(state + 4 * npix + 4 * p);
     double sum[3] = {0.0, 0.0, 0.0}, bias[3] = {0.0, 0.0, 0.0}, w = 0.0, wb = 0.0;
     if (accumulate) {
-        for (int k = 0; k < 3; ++k) {
-            sum[k] = state[p * 8 + k];
-            bias[k] = state[p * 8 + 3 + k];
-        }
-        w = state[p * 8 + 6];
-        wb = state[p * 8 + 7];
+        const d2 s0 = rs[0], s1 = rs[1], b0 = rb[0], b1 = rb[1];
+        sum[0] = s0.x; sum[1] = s0.y; sum[2] = s1.x; w = s1.y;
+        bias[0] = b0.x; bias[1] = b0.y; bias[2] = b1.x; wb = b1.y;
     }
     // update_pixel for one sample (the Kahan chain is sequential in s)
     auto update = [&](const double c[3]) {
@@ -1466,6 +1201,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             // final photon {wavelength, intensity}: one 16-B non-temporal load
+            VR_GUARD(s + j, p);
             v[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p));
             dark = dark && __double_as_longlong(v[j].x) == 0 && __double_as_longlong(v[j].y) == 0;
         }
@@ -1490,6 +1226,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
         for (uint32_t j = 0; j < kB; ++j) update(c[j]);
     }
     for (; s < spp; ++s) {
+        VR_GUARD(s, p);
         const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)s * npix + p));
         const double wl = v.x, I = v.y;
         const double Is = I * 360.0;
@@ -1497,13 +1234,12 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
         const double c[3] = {cx.x * Is, cx.y * Is, cx.z * Is};
         update(c);
     }
-    for (int k = 0; k < 3; ++k) {
-        state[p * 8 + k] = sum[k];
-        state[p * 8 + 3 + k] = bias[k];
-    }
-    state[p * 8 + 6] = w;
-    state[p * 8 + 7] = wb;
+    rs[0] = d2{sum[0], sum[1]};
+    rs[1] = d2{sum[2], w};
+    rb[0] = d2{bias[0], bias[1]};
+    rb[1] = d2{bias[2], wb};
 }
+#undef VR_GUARD
 
 template <int STACK>
 __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
@@ -1550,15 +1286,16 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     const uint64_t items = dev::render_items(a, ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64);
     const uint64_t want = (items + 255) / 256;
     dim3 grid((unsigned)(want < (uint64_t)grid_limit ? want : (uint64_t)grid_limit)), block(256);
-    // experiment hook (tools/variants.py): 1..4 = force that many waves per SIMD (default 3)
-    const char* ve = getenv("VR_KERNEL_VARIANT");
-    const int variant = ve ? atoi(ve) : 0;
-    (void)variant;
     // kinds present (bit 0 Lambertian, 1 reflective, 2 Phong or dielectric) -> specialisation:
     // Lambertian-only (1), reflective-only (2) or the general kernel (3)
     mats = (mats == 1 || mats == 2) ? mats : 3;
     if (!dark0) mats = 3;  // the general kernel
-    if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);  // experiment hook
+#ifdef VR_TUNING_VARIANTS  // experiment hooks of tuning builds only (tools/variants.py)
+    // 1..4 = force that many waves per SIMD (default 3); VR_FORCE_MATS: the material specialisation
+    const char* ve = getenv("VR_KERNEL_VARIANT");
+    const int variant = ve ? atoi(ve) : 0;
+    if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);
+#endif
     if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
         if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
         else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
@@ -1571,7 +1308,8 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
         }
         const uint64_t npix = a.tile_width * a.tile_height;
         hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
-                           (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width);
+                           (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width,
+                       a.stage_tag, a.stage_gen, a.error_flag);
         return hipGetLastError();
     }
 #define VR_LAUNCH(C, R, D, M, W)                                                                      \
@@ -1610,7 +1348,8 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     }
     const uint64_t npix = a.tile_width * a.tile_height;
     hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
-                       (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width);
+                       (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width,
+                       a.stage_tag, a.stage_gen, a.error_flag);
     return hipGetLastError();
 }
 

@@ -3,8 +3,9 @@
 The path is embarrassingly parallel over (pixel, sample).  Rank r of N renders the whole tile for
 sample indices [(step * N + r) * spp, +spp) -- the counter-based random stream
 makes the union over ranks exactly the sample set of a one-GPU render of N * spp samples -- and
-the per-pixel accumulation records (8 f64: sum XYZ, Kahan bias XYZ, weight, weight bias) are
-summed onto rank 0 with one collective (RCCL over xGMI on MI355X, gloo on CPU in the tests).
+the merge-exact half of the per-pixel accumulation records ({sum X, Y, Z, weight}, contiguous:
+vanrijn_amd/records.py) is summed onto rank 0 with one in-place collective (RCCL over xGMI on
+MI355X, gloo on CPU in the tests).
 Summing records merges disjoint sample sets the way AccumulationBuffer::merge_tile's weighted
 blend does (accumulation_buffer.rs:62-85): mean = sum(colour_sum) / sum(weight).
 
@@ -14,9 +15,7 @@ blend does (accumulation_buffer.rs:62-85): mean = sum(colour_sum) / sum(weight).
 import torch
 import torch.distributed as dist
 
-RECORD = 8  # f64 per pixel
-SUMS = (0, 1, 2, 6)  # the merge-exact part of a record: sum X, Y, Z and the weight (32 B per pixel)
-BIAS_COLUMNS = (3, 4, 5, 7)  # Kahan compensations of the XYZ sums and of the weight
+from . import records as R
 
 
 def world_info(group=None):
@@ -43,44 +42,43 @@ def shard_spp(total_spp, world, split):
 
 def reduce_bytes(state: torch.Tensor):
     """Bytes one rank contributes to the reduce: the 4 f64 sums of every pixel."""
-    return state.numel() // RECORD * len(SUMS) * state.element_size()
+    return R.sums(state).numel() * state.element_size()
 
 
 def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None):
     """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path).
 
-    Only the merge-exact sums {sum X, sum Y, sum Z, weight} travel -- 32 B per pixel, half the
-    record: they are gathered into one packed buffer, reduced, and scattered back on `dst`.  The
-    Kahan compensations belong to no single update_pixel sequence once sums of different ranks are
-    added (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
-    reduced state starts a fresh compensated sum from the merged totals.  Other ranks keep their
-    own records.  `timer`: a list that receives (start, end) CUDA events around the collective."""
+    Only the merge-exact sums {sum X, sum Y, sum Z, weight} travel -- 32 B per pixel, the records'
+    first half, contiguous, reduced in place (no gather or scatter copies).  The Kahan
+    compensations belong to no single update_pixel sequence once sums of different ranks are added
+    (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
+    reduced state starts a fresh compensated sum from the merged totals.  On the other ranks the
+    sums half belongs to the collective once called (in place: gloo uses it as scratch; the frame
+    is done with it), their compensations are untouched.  `timer`: a list that receives (start, end) CUDA events around everything this
+    call enqueues (the collective and the zeroing)."""
     rank, world = world_info(group)
     # through the collective whenever a group exists (at world size 1 too: bench.py under
     # torch.distributed.run on one GPU rehearses the RCCL step the 8-GPU runs take)
     if dist.is_available() and dist.is_initialized():
-        s = state.view(-1, RECORD)
-        cols = torch.tensor(SUMS, device=state.device)
-        packed = s.index_select(1, cols)  # [pixels][4], contiguous
+        flat = state.view(-1)
+        sums = flat[:R.sums(flat).numel()]  # a contiguous view: the collective's buffer
         ev = None
         if timer is not None and state.is_cuda:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        dist.reduce(packed, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        dist.reduce(sums, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if rank == dst:
+            R.compensations(flat).zero_()
         if ev is not None:
             ev[1].record()
             timer.append(ev)
-        if rank == dst:
-            s.index_copy_(1, cols, packed)
-            s[:, 3:6] = 0.0
-            s[:, 7] = 0.0
     return state
 
 
 def mean_colour(state: torch.Tensor):
-    """Mean XYZ [.., 3] of records [.., 8] (accumulation_buffer.rs:59: sum * (1 / weight))."""
-    s = state.reshape(-1, RECORD)
-    w = s[:, 6:7]
+    """Mean XYZ [pixels, 3] of records (accumulation_buffer.rs:59: sum * (1 / weight))."""
+    s = R.sums(state)
+    w = s[:, 3:4]
     return torch.where(w != 0, s[:, 0:3] * (1.0 / w), torch.zeros_like(s[:, 0:3]))
 
 

@@ -16,6 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _native as N
+from . import records as R
 
 RECURSION_LIMIT = 128  # camera.rs:69
 SAMPLE_RECORD_DTYPE = np.dtype([("wavelength", "<f8"), ("intensity", "<f8"), ("xyz", "<f8", (3,)),
@@ -162,18 +163,17 @@ class AccumulationBuffer:
         return ImageRgbU8(out)
 
     @staticmethod
-    def from_state(state):
-        """Build from device-state records [h][w][8] = {sum XYZ, bias XYZ, weight, weight_bias}."""
-        s = np.asarray(state, dtype=np.float64)
-        h, w = s.shape[:2]
-        b = AccumulationBuffer(w, h)
-        b.colour_sum_buffer[...] = s[..., 0:3]
-        b.colour_bias_buffer[...] = s[..., 3:6]
-        b.weight_buffer[...] = s[..., 6]
-        b.weight_bias_buffer[...] = s[..., 7]
-        wgt = s[..., 6:7]
+    def from_state(state, width, height):
+        """Build from a tile's device-state records (vanrijn_amd/records.py layout)."""
+        f = R.fields(state, (height, width))
+        b = AccumulationBuffer(width, height)
+        b.colour_sum_buffer[...] = f["colour_sum"]
+        b.colour_bias_buffer[...] = f["colour_bias"]
+        b.weight_buffer[...] = f["weight"]
+        b.weight_bias_buffer[...] = f["weight_bias"]
+        wgt = f["weight"][..., None]
         with np.errstate(divide="ignore", invalid="ignore"):
-            b.colour_buffer[...] = np.where(wgt != 0.0, s[..., 0:3] * (1.0 / wgt), 0.0)
+            b.colour_buffer[...] = np.where(wgt != 0.0, f["colour_sum"] * (1.0 / wgt), 0.0)
         return b
 
 
@@ -231,15 +231,16 @@ def trace_rays(scene, origins, directions, device=0):
 
 
 def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample, state_ptr, stream_ptr=None,
-                       accumulate=False, timed=False, counters=False, device=0, defer_times=False):
-    """Enqueue a render into device state records (8 f64 per pixel) at `state_ptr` (a device
-    pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel time when timed;
-    `defer_times`: the events are recorded without waiting, read by collect_launch_times)."""
+                       accumulate=False, timed=False, counters=False, device=0, defer_times=False, cull=True):
+    """Enqueue a render into device state records (8 f64 per pixel, vanrijn_amd/records.py) at
+    `state_ptr` (a device pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel
+    time when timed; `defer_times`: the events are recorded without waiting, read by
+    collect_launch_times; `cull=False`: every sample traced, VR_LAUNCH_NO_CULL)."""
     ds = _scene_handle(scene, device)
     p = _params(tile, height, width, spp, seed, first_sample, accumulate)
     st = N.LaunchStats()
     flags = (N.LAUNCH_TIMED if timed or defer_times else 0) | (N.LAUNCH_COUNTERS if counters else 0) | \
-        (N.LAUNCH_DEFER_TIMES if defer_times else 0)
+        (N.LAUNCH_DEFER_TIMES if defer_times else 0) | (0 if cull else N.LAUNCH_NO_CULL)
     N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
                                           C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
     return st.as_dict()
@@ -263,10 +264,11 @@ def stream_check_error(scene, stream_ptr=None, device=0):
 
 
 def resolve_state(state):
-    """Mean XYZ [.., 3] of state records [.., 8] (accumulation_buffer.rs:59)."""
-    s = np.ascontiguousarray(state, dtype=np.float64)
-    out = np.zeros(s.shape[:-1] + (3,))
-    N.check(N.lib().vr_resolve_state(s.ctypes.data_as(C.c_void_p), s.size // 8, out.ctypes.data_as(C.c_void_p)))
+    """Mean XYZ [pixels, 3] of flat state records (accumulation_buffer.rs:59)."""
+    s = np.ascontiguousarray(np.asarray(state, dtype=np.float64).reshape(-1))
+    n = R.pixels(s)
+    out = np.zeros((n, 3))
+    N.check(N.lib().vr_resolve_state(s.ctypes.data_as(C.c_void_p), n, out.ctypes.data_as(C.c_void_p)))
     return out
 
 
@@ -299,6 +301,6 @@ class ImageRgbU8:
 
 
 def tone_map_device(state_ptr, pixel_count, rgb_ptr, stream_ptr=None, device=0):
-    """Device records (8 f64 per pixel) -> device RGB bytes (3 per pixel), enqueued on a stream."""
+    """Device records (vanrijn_amd/records.py) -> device RGB bytes (3 per pixel), on a stream."""
     N.check(N.lib().vr_tone_map_device(C.c_void_p(state_ptr), pixel_count, C.c_void_p(rgb_ptr), device,
                                        C.c_void_p(stream_ptr or 0)))

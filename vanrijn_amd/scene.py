@@ -13,13 +13,25 @@ A `Scene` lowers to a plain-data `SceneSpec` (numbers only) which the C ABI cons
 (`vr_scene_create`) -- and which the test oracle consumes too, so both see identical inputs.
 """
 from dataclasses import dataclass, field
+import atexit
 import ctypes as C
 from enum import Enum
 from typing import List
+import weakref
 
 import numpy as np
 
 from . import _native as N
+
+# every DeviceScene not yet released: destroyed at interpreter exit while the library and the HIP
+# runtime are still loaded (module teardown order would otherwise decide)
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _release_live_scenes():
+    for s in list(_LIVE):
+        s.release()
 
 SHORTEST_VISIBLE_WAVELENGTH = 380.0  # src/colour/mod.rs:13
 LONGEST_VISIBLE_WAVELENGTH = 740.0   # src/colour/mod.rs:14
@@ -304,10 +316,11 @@ class DeviceScene:
     """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
 
     def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False, reference_bvh=False,
-                 device_sah=False):
+                 device_sah=False, greedy_collapse=False):
         """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH: the reference's tree);
         reference_bvh: traverse the reference's median-split tree instead of the SAH tree;
-        device_sah: build the SAH traversal tree on the GPU too (VR_SCENE_DEVICE_SAH)."""
+        device_sah: build the SAH traversal tree on the GPU too (VR_SCENE_DEVICE_SAH);
+        greedy_collapse: the greedy 4-wide collapse instead of the SAH-optimal one (inspection)."""
         L = N.lib()
         self.spec = spec
         keep = []  # keep ctypes buffers alive during vr_scene_create
@@ -353,17 +366,31 @@ class DeviceScene:
                            mats, prim_arr, mesh_arr, obj_arr, C.pointer(ig) if ig is not None else None)
         h = C.c_void_p()
         flags = ((N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0) |
-                 (N.SCENE_REFERENCE_BVH if reference_bvh else 0) | (N.SCENE_DEVICE_SAH if device_sah else 0))
+                 (N.SCENE_REFERENCE_BVH if reference_bvh else 0) | (N.SCENE_DEVICE_SAH if device_sah else 0) |
+                 (N.SCENE_GREEDY_COLLAPSE if greedy_collapse else 0))
         N.check(L.vr_scene_create(C.byref(desc), device, flags, C.byref(h)))
         self.handle = h
         self.device = device
         self.host_only = host_only
+        # bound now: at interpreter exit module globals (N, N.lib) may already be torn down when
+        # __del__ runs; scenes still alive then are released by _release_live_scenes (atexit)
+        self._destroy = L.vr_scene_destroy
+        _LIVE.add(self)
 
-    def __del__(self):
+    def release(self):
+        """vr_scene_destroy now (waits for the scene's queued work); idempotent."""
         h = getattr(self, "handle", None)
         if h:
-            N.lib().vr_scene_destroy(h)
             self.handle = None
+            self._destroy(h)
+
+    def __del__(self):
+        self.release()
+
+    def set_staging_limit(self, nbytes):
+        """vr_scene_set_staging_limit: cap one call's staging memory (0: half the free HBM); larger
+        frames run in several launches with bit-identical records."""
+        N.check(N.lib().vr_scene_set_staging_limit(self.handle, int(nbytes)))
 
     def info(self):
         i = N.SceneInfo()
