@@ -49,6 +49,23 @@ for s in $STEPS; do
           --master-port 29517 bench.py --config $cfg --gpus 1 --steps 2 --warmup 1 --no-cpu-baseline --no-drop-in \
           > gpurun_out/${TAG}_dist_$cfg.json 2> gpurun_out/${TAG}_dist_$cfg.err
       rc=$?; echo "dist $cfg rc=$rc"; cut -c 1-300 gpurun_out/${TAG}_dist_$cfg.json; tail -3 gpurun_out/${TAG}_dist_$cfg.err ;;
+    ab)
+      # alternating-process A/B of the libraries in $AB_LIBS (tools/ab.sh; ROUNDS, SCENES)
+      timeout -k 10 1200 bash tools/ab.sh $AB_LIBS > gpurun_out/${TAG}_ab.txt 2>&1
+      rc=$?; echo "ab rc=$rc"; tail -20 gpurun_out/${TAG}_ab.txt; cp gpurun_out/ab_libs.jsonl gpurun_out/${TAG}_ab_libs.jsonl ;;
+    benchab)
+      # bench.py --config $cfg with each library of $AB_LIBS in turn, ROUNDS rounds (no PMC / CPU legs)
+      : > gpurun_out/${TAG}_benchab_$cfg.jsonl
+      for r in $(seq 1 ${ROUNDS:-3}); do
+        for L in $AB_LIBS; do
+          VR_LIBRARY=$L timeout -k 10 300 python bench.py --config $cfg --steps ${AB_STEPS:-10} --warmup 2 \
+              --no-cpu-baseline --no-drop-in --no-pmc 2>> gpurun_out/${TAG}_benchab.err | \
+              python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().split(chr(10))[-1]); print(json.dumps({'lib': '$L', 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['roofline']['kernel_ms'], 'value': d['value']}))" \
+              >> gpurun_out/${TAG}_benchab_$cfg.jsonl
+          rc=$?; [ $rc -eq 0 ] || break 2
+        done
+      done
+      echo "benchab $cfg rc=$rc"; cat gpurun_out/${TAG}_benchab_$cfg.jsonl ;;
     libtests)
       # the GPU tests against another build of the library (abx/lib$cfg.so, e.g. the VR_STAGE_GUARD build)
       VR_LIBRARY=abx/lib$cfg.so timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 \

@@ -618,6 +618,10 @@ struct CallCtx {
 // Environment overrides exist in tuning builds only (python -m vanrijn_amd.build with VR_TUNING=1,
 // -DVR_TUNING_VARIANTS: tools/variants.py threshold sweeps, tools/cycles.py diagnostics); a default
 // build reads no VR_* variable, so nothing in a user's environment changes rendering or timing.
+// launch defaults (A/B builds may override them at compile time)
+#ifndef VR_LEAF_THRESHOLD_DEFAULT  // a leaf round once this many entries are queued (or lanes stall)
+#define VR_LEAF_THRESHOLD_DEFAULT 48u
+#endif
 static const char* tuning_env(const char* name) {
 #ifdef VR_TUNING_VARIANTS
     return getenv(name);
@@ -779,8 +783,13 @@ int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render
 // surface area from the root (a child's box lies inside its parent's, so the set is a connected
 // top of the tree, and visits are roughly proportional to area); the other nodes keep their
 // depth-first order.  Only indices change: the walk, and so every result, is the same.
-int hot_node_budget() {
-    static const int k = tuning_env("VR_HOT_NODES") ? std::max(0, atoi(tuning_env("VR_HOT_NODES"))) : vr::kHotNodesDefault;
+// Per scene: on for trees of at most kHotTreeMax wide nodes (the bunny-sized
+// scenes, whose rays spend a larger share of their node steps in the top levels), off for large
+// meshes (C5: the LDS copy there only cost its setup, +3 %); the render kernel has a HOT
+// instantiation for it.
+int hot_node_budget(size_t wide_nodes) {
+    int k = wide_nodes <= (size_t)vr::kHotTreeMax ? vr::kHotNodesMax : 0;
+    if (const char* e = tuning_env("VR_HOT_NODES")) k = std::max(0, atoi(e));
     return std::min(k, vr::kHotNodesMax);
 }
 
@@ -891,7 +900,7 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
         std::fprintf(stderr, "vr wide tree: %zu nodes, stack %d, sum SA / SA(first root) %.4f (%s collapse)\n",
                      s->nodes4.size(), s->wide_stack, sum / root, use_dp ? "DP" : "greedy");
     }
-    s->dev.hot_count = hot_prefix(s->nodes4, s->bvhs, hot_node_budget());
+    s->dev.hot_count = hot_prefix(s->nodes4, s->bvhs, hot_node_budget(s->nodes4.size()));
 }
 
 template <class T>
@@ -1106,7 +1115,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
     }
     const char* lt = tuning_env("VR_LEAF_THRESHOLD");  // tuning hooks
-    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
+    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : VR_LEAF_THRESHOLD_DEFAULT;
     const char* ls = tuning_env("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
     const char* lf = tuning_env("VR_LEAF_FEW");  // tuning hook (0: off)

@@ -15,13 +15,13 @@ constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
 // VR_LAUNCH_DEFER_TIMES launches a stream may hold before vr_collect_launch_times (3 HIP events each)
 constexpr uint32_t kMaxDeferredLaunches = 4096;
 // LDS copy of the top of the 4-wide tree (DeviceScene::hot_count nodes, at most kHotNodesMax:
-// 4 KB of the render kernel's LDS per workgroup at 32); VR_HOT_NODES at scene creation lowers the
-// count.  Measured and rejected: off unless built with -DVR_HOT_MAX=16 / 32
-#ifndef VR_HOT_MAX
-#define VR_HOT_MAX 0
+// 4 KB of the render kernel's LDS per workgroup), for scenes whose largest 4-wide tree has at most
+// kHotTreeMax nodes (vr_host.cpp hot_node_budget: DESIGN.md section 6)
+constexpr int kHotNodesMax = 32;
+#ifndef VR_HOT_TREE_MAX
+#define VR_HOT_TREE_MAX 100000
 #endif
-constexpr int kHotNodesMax = VR_HOT_MAX;
-constexpr int kHotNodesDefault = VR_HOT_MAX;
+constexpr int kHotTreeMax = VR_HOT_TREE_MAX;
 
 // One interior node of a binary BVH, child boxes stored in the parent so a visit tests both
 // children with one 128-B record.  box[c] = {min x, max x, min y, max y, min z, max z} of child c
