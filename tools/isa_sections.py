@@ -14,7 +14,9 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "_ZN2vr3dev13render_kernelILi32ELb0ELb0ELb1ELi1ELi3ELb0EEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
+# the C3 timed kernel: STACK 32, Lambertian-only, DARK0, the LDS tree top (HOT = 32; VR_ISA_HOT=0: without)
+KERNEL = ("_ZN2vr3dev13render_kernelILi32ELb0ELb0ELb1ELi1ELi3ELb0ELi%sEEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
+          % os.environ.get("VR_ISA_HOT", "32"))
 
 
 def cost(op):

@@ -72,6 +72,10 @@ class _OutputPool:
         self.keep = keep
         self.lock = threading.Lock()
         self.stores = []  # backing arrays
+        # the reference count of a store nothing but the pool refers to, measured on this
+        # interpreter (how many temporaries getrefcount itself sees differs between versions)
+        probe = [np.empty(1)]
+        self._free_refs = sys.getrefcount(probe[0])
 
     @staticmethod
     def _split(store, width, height):
@@ -81,8 +85,8 @@ class _OutputPool:
                 store[10 * n:11 * n].reshape(height, width))
 
     def _free(self, i):
-        # references: the pool's list and getrefcount's own argument; any live view adds its .base
-        return sys.getrefcount(self.stores[i]) <= 2
+        # references: the pool's list (and getrefcount's own); any live view adds its .base
+        return sys.getrefcount(self.stores[i]) <= self._free_refs
 
     def views(self, width, height):
         size = 11 * width * height
