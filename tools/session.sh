@@ -60,7 +60,7 @@ for s in $STEPS; do
         for L in $AB_LIBS; do
           VR_LIBRARY=$L timeout -k 10 300 python bench.py --config $cfg --steps ${AB_STEPS:-10} --warmup 2 \
               --no-cpu-baseline --no-drop-in --no-pmc 2>> gpurun_out/${TAG}_benchab.err | \
-              python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().split(chr(10))[-1]); print(json.dumps({'lib': '$L', 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['roofline']['kernel_ms'], 'value': d['value']}))" \
+              python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().split(chr(10))[-1]); print(json.dumps({'lib': '$L', 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['roofline']['kernel_ms'], 'reduce_ms': d['roofline'].get('reduce_kernel_ms'), 'value': d['value']}))" \
               >> gpurun_out/${TAG}_benchab_$cfg.jsonl
           rc=$?; [ $rc -eq 0 ] || break 2
         done

@@ -618,10 +618,6 @@ struct CallCtx {
 // Environment overrides exist in tuning builds only (python -m vanrijn_amd.build with VR_TUNING=1,
 // -DVR_TUNING_VARIANTS: tools/variants.py threshold sweeps, tools/cycles.py diagnostics); a default
 // build reads no VR_* variable, so nothing in a user's environment changes rendering or timing.
-// launch defaults (A/B builds may override them at compile time)
-#ifndef VR_LEAF_THRESHOLD_DEFAULT  // a leaf round once this many entries are queued (or lanes stall)
-#define VR_LEAF_THRESHOLD_DEFAULT 48u
-#endif
 static const char* tuning_env(const char* name) {
 #ifdef VR_TUNING_VARIANTS
     return getenv(name);
@@ -777,84 +773,6 @@ namespace {
 int stack_depth(const vr_scene* s) { return std::max(1, s->max_depth - 1); }  // binary tree walks
 int wide_stack_depth(const vr_scene* s) { return s->wide_stack + 1; }  // render kernel (+1: branchless pushes)
 
-// Hot prefix: the top of the largest BVH's 4-wide tree moves to nodes4[0 .. k), which the render
-// kernel copies into LDS once per workgroup and reads from there (every ray that enters the BVH
-// starts its chain of dependent node fetches at the root).  The k nodes are chosen greedily by
-// surface area from the root (a child's box lies inside its parent's, so the set is a connected
-// top of the tree, and visits are roughly proportional to area); the other nodes keep their
-// depth-first order.  Only indices change: the walk, and so every result, is the same.
-// Per scene: on for trees of at most kHotTreeMax wide nodes (the bunny-sized
-// scenes, whose rays spend a larger share of their node steps in the top levels), off for large
-// meshes (C5: the LDS copy there only cost its setup, +3 %); the render kernel has a HOT
-// instantiation for it.
-int hot_node_budget(size_t wide_nodes) {
-    int k = wide_nodes <= (size_t)vr::kHotTreeMax ? vr::kHotNodesMax : 0;
-    if (const char* e = tuning_env("VR_HOT_NODES")) k = std::max(0, atoi(e));
-    return std::min(k, vr::kHotNodesMax);
-}
-
-int hot_prefix(std::vector<vr::Node4>& n4, std::vector<vr::Bvh>& bvhs, int k) {
-    if (k <= 0 || n4.empty()) return 0;
-    // the BVH with the most wide nodes (each subtree is a contiguous depth-first range)
-    int32_t root = -1;
-    size_t most = 0;
-    for (const auto& b : bvhs) {
-        if (b.root4 < 0) continue;
-        size_t cnt = 0;
-        std::vector<int32_t> st{b.root4};
-        while (!st.empty()) {
-            const int32_t x = st.back();
-            st.pop_back();
-            ++cnt;
-            for (int c = 0; c < 4; ++c)
-                if (n4[x].child[c] >= 0) st.push_back(n4[x].child[c]);
-        }
-        if (cnt > most) {
-            most = cnt;
-            root = b.root4;
-        }
-    }
-    if (root < 0) return 0;
-    auto area = [](const float* b) {
-        const double dx = (double)b[1] - b[0], dy = (double)b[3] - b[2], dz = (double)b[5] - b[4];
-        return (dx >= 0.0 && dy >= 0.0 && dz >= 0.0) ? dx * dy + dy * dz + dz * dx : 0.0;
-    };
-    std::vector<int32_t> hot{root};
-    std::vector<std::pair<double, int32_t>> frontier;  // (area, node) of hot nodes' interior children
-    auto expand = [&](int32_t x) {
-        for (int c = 0; c < 4; ++c)
-            if (n4[x].child[c] >= 0) frontier.push_back({area(n4[x].box[c]), n4[x].child[c]});
-    };
-    expand(root);
-    while ((int)hot.size() < k && !frontier.empty()) {
-        size_t bi = 0;  // largest area; ties: the earlier node (deterministic)
-        for (size_t i = 1; i < frontier.size(); ++i)
-            if (frontier[i].first > frontier[bi].first ||
-                (frontier[i].first == frontier[bi].first && frontier[i].second < frontier[bi].second))
-                bi = i;
-        const int32_t x = frontier[bi].second;
-        frontier.erase(frontier.begin() + (ptrdiff_t)bi);
-        hot.push_back(x);
-        expand(x);
-    }
-    const int32_t n = (int32_t)n4.size();
-    std::vector<int32_t> perm(n, -1);
-    for (int32_t i = 0; i < (int32_t)hot.size(); ++i) perm[hot[i]] = i;
-    int32_t next = (int32_t)hot.size();
-    for (int32_t i = 0; i < n; ++i)
-        if (perm[i] < 0) perm[i] = next++;
-    std::vector<vr::Node4> out(n);
-    for (int32_t i = 0; i < n; ++i) {
-        vr::Node4 w = n4[i];
-        for (int c = 0; c < 4; ++c)
-            if (w.child[c] >= 0) w.child[c] = perm[w.child[c]];
-        out[perm[i]] = w;
-    }
-    n4.swap(out);
-    for (auto& b : bvhs)
-        if (b.root4 >= 0) b.root4 = perm[b.root4];
-    return (int)hot.size();
-}
 
 // the render kernel's 4-wide tree over every traversed mesh's binary tree `nodes`
 void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
@@ -900,7 +818,6 @@ void collapse_wide(vr_scene* s, const std::vector<vr::Node>& nodes) {
         std::fprintf(stderr, "vr wide tree: %zu nodes, stack %d, sum SA / SA(first root) %.4f (%s collapse)\n",
                      s->nodes4.size(), s->wide_stack, sum / root, use_dp ? "DP" : "greedy");
     }
-    s->dev.hot_count = hot_prefix(s->nodes4, s->bvhs, hot_node_budget(s->nodes4.size()));
 }
 
 template <class T>
@@ -1115,7 +1032,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
     }
     const char* lt = tuning_env("VR_LEAF_THRESHOLD");  // tuning hooks
-    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : VR_LEAF_THRESHOLD_DEFAULT;
+    a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
     const char* ls = tuning_env("VR_LEAF_STALL");
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
     const char* lf = tuning_env("VR_LEAF_FEW");  // tuning hook (0: off)

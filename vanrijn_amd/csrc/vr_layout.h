@@ -14,14 +14,6 @@ constexpr int kMaxSpectrumSamples = 64;
 constexpr double kBounceBias = 0.0000001;  // simple_random_integrator.rs:42
 // VR_LAUNCH_DEFER_TIMES launches a stream may hold before vr_collect_launch_times (3 HIP events each)
 constexpr uint32_t kMaxDeferredLaunches = 4096;
-// LDS copy of the top of the 4-wide tree (DeviceScene::hot_count nodes, at most kHotNodesMax:
-// 4 KB of the render kernel's LDS per workgroup), for scenes whose largest 4-wide tree has at most
-// kHotTreeMax nodes (vr_host.cpp hot_node_budget: DESIGN.md section 6)
-constexpr int kHotNodesMax = 32;
-#ifndef VR_HOT_TREE_MAX
-#define VR_HOT_TREE_MAX 100000
-#endif
-constexpr int kHotTreeMax = VR_HOT_TREE_MAX;
 
 // One interior node of a binary BVH, child boxes stored in the parent so a visit tests both
 // children with one 128-B record.  box[c] = {min x, max x, min y, max y, min z, max z} of child c
@@ -135,11 +127,6 @@ struct DeviceScene {
     int32_t light_base;
     int32_t sky_row;       // materials[sky_row]: knots / inv_step of the RGB basis (the sky lookup)
     const double* light_dirs;
-    // nodes4[0 .. hot_count): the top of the largest BVH's 4-wide tree (its root and the children
-    // with the largest boxes, greedily), which the render kernel copies into LDS once per
-    // workgroup (vr_host.cpp hot_prefix); 0: none
-    int32_t hot_count;
-    int32_t pad_hot;
 };
 
 struct RenderArgs {

@@ -141,10 +141,7 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
-// HOT: the top of the largest BVH's 4-wide tree is copied into LDS per workgroup (0: not; a per-
-// scene choice by tree size, vr_host.cpp hot_node_budget).
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          int HOT = 0>
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -165,15 +162,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
     const int tid = threadIdx.x;
     const unsigned lane = __lane_id();
-    // the top of the largest BVH's 4-wide tree (nodes4[0 .. hot_count), vr_host.cpp hot_prefix),
-    // copied once per workgroup: every ray entering that BVH starts its chain of dependent node
-    // fetches there, and those steps read LDS instead of L1 / L2
-    __shared__ uint4 hot4[(HOT > 0 ? HOT : 1) * 8];
-    const uint32_t hot_n = HOT > 0 ? (uint32_t)min(A.scene.hot_count, HOT) : 0u;
-    if constexpr (HOT > 0) {
-        for (uint32_t i = tid; i < hot_n * 8; i += 256) hot4[i] = reinterpret_cast<const uint4*>(A.scene.nodes4)[i];
-        __syncthreads();
-    }
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
     lr_key[tid] = 0;
     lr_cnt[tid] = 0;
@@ -831,28 +819,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             if (state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
-                // the node's 112 B (boxes, links): from LDS for the hot top of the tree (HOT)
-                union NodeWords {
-                    uint4 q[7];
-                    struct {
-                        float box[4][6];
-                        int32_t child[4];
-                    } n;
-                };
-                NodeWords nu;
-                if constexpr (HOT > 0) {
-                    if ((uint32_t)node < hot_n) {
-#pragma unroll
-                        for (int j = 0; j < 7; ++j) nu.q[j] = hot4[node * 8 + j];
-                    } else {
-                        const uint4* gq = reinterpret_cast<const uint4*>(VR_NODES4 + node);
-#pragma unroll
-                        for (int j = 0; j < 7; ++j) nu.q[j] = gq[j];
-                    }
-                }
-                // the rest of the step reads the node through `nd` (global memory, or the LDS copy);
-                // HOT is a compile-time constant, so HOT = 0 reads the Node4 record directly
-                const Node4& nd = HOT > 0 ? *reinterpret_cast<const Node4*>(&nu) : VR_NODES4[node];
+                const Node4& nd = VR_NODES4[node];
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
@@ -1070,10 +1037,7 @@ __global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Pri
             clear = sphere_clear(c, pr.scalar);
         }
     }
-    // the BVH roots: whether the block's camera rays may meet a mesh at all (`mesh`, the priority
-    // below) and, while no primitive has kept the block, whether they all miss every mesh
-    bool mesh = false;
-    for (int i = 0; i < A.scene.bvh_count; ++i) {
+    for (int i = 0; i < A.scene.bvh_count && clear; ++i) {
         const Bvh& bv = bvhs[i];
         if (bv.root4 == INT32_MIN) continue;  // an empty mesh never hits
         const double* bb = bv.root_box;
@@ -1096,47 +1060,32 @@ __global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Pri
         }
         const V3 c = mk(0.5 * (bb[0] + bb[1]), 0.5 * (bb[2] + bb[3]), 0.5 * (bb[4] + bb[5]));
         const V3 e = mk(bb[1] - bb[0], bb[3] - bb[2], bb[5] - bb[4]);
-        if (!sphere_clear(c, 0.5 * sqrt(dot(e, e)) * (1.0 + 1e-9) + 1e-12)) mesh = true;
+        clear = sphere_clear(c, 0.5 * sqrt(dot(e, e)) * (1.0 + 1e-9) + 1e-12);
     }
-    if (mesh) clear = false;
-    // bit 0: culled (every sample is the photon {0, 0}); bit 1: live and may meet a mesh -- its
-    // samples are handed out first (block_compact_kernel): the longest paths start earliest
-    mask[b] = clear ? 1 : (mesh ? 2 : 0);
+    mask[b] = clear ? 1 : 0;
 }
 
-// The live blocks of a cull mask (one workgroup: each thread counts a contiguous run of blocks, an
-// LDS scan gives the runs' offsets, then each thread writes its run's live ones): first the blocks
-// whose camera rays may meet a mesh (mask bit 1), then the others, each in block order.  Work items
-// are numbered sample-major over this list, so within every sample round the blocks with the long
-// (mesh-bouncing) paths go out first and the launch's tail is made of the short ones.  The order
-// changes which lane traces a sample, never its result (the random stream is counter-based and the
-// reduce is ordered by sample).
+// The live blocks of a cull mask in block order (one workgroup: each thread counts a contiguous
+// run of blocks, an LDS scan gives the runs' offsets, then each thread writes its run's live ones).
 __global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask, uint32_t n, uint32_t* live,
                                                               uint32_t* count) {
-    __shared__ uint32_t part[2][1024];
+    __shared__ uint32_t part[1024];
     const uint32_t tid = threadIdx.x, per = (n + 1023) / 1024;
     const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
-    uint32_t c[2] = {0, 0};  // [0]: live, may meet a mesh; [1]: other live blocks
-    for (uint32_t i = lo; i < hi; ++i) {
-        c[0] += mask[i] == 2;
-        c[1] += mask[i] == 0;
-    }
-    part[0][tid] = c[0];
-    part[1][tid] = c[1];
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i) c += mask[i] == 0;
+    part[tid] = c;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scans
-        const uint32_t v0 = tid >= d ? part[0][tid - d] : 0u, v1 = tid >= d ? part[1][tid - d] : 0u;
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+        const uint32_t v = tid >= d ? part[tid - d] : 0u;
         __syncthreads();
-        part[0][tid] += v0;
-        part[1][tid] += v1;
+        part[tid] += v;
         __syncthreads();
     }
-    uint32_t off0 = part[0][tid] - c[0], off1 = part[0][1023] + part[1][tid] - c[1];
-    for (uint32_t i = lo; i < hi; ++i) {
-        if (mask[i] == 2) live[off0++] = i;
-        else if (mask[i] == 0) live[off1++] = i;
-    }
-    if (tid == 1023) *count = part[0][1023] + part[1][1023];
+    uint32_t off = part[tid] - c;
+    for (uint32_t i = lo; i < hi; ++i)
+        if (mask[i] == 0) live[off++] = i;
+    if (tid == 1023) *count = part[1023];
 }
 
 #ifndef VR_REDUCE_BATCH  // samples whose colours the ordered reduce computes together
@@ -1203,7 +1152,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     uint32_t s = 0;
     if (mask) {
         const uint64_t py = p / tile_width, px = p - py * tile_width;
-        if (mask[(py >> 3) * ((tile_width + 7) >> 3) + (px >> 3)] & 1) {
+        if (mask[(py >> 3) * ((tile_width + 7) >> 3) + (px >> 3)]) {
             // a culled block (block_cull_kernel): every sample is the photon {0, 0}, colour +0.
             // From a fresh record the Kahan chain has a closed form: colour y = +0 * 1 - +0 = +0
             // keeps sums and compensations +0, and the weight counts 1, 2, .., spp exactly with
@@ -1219,15 +1168,20 @@ __global__ __launch_bounds__(256) void accumulate_kernel(double* state, const do
     for (; s + kB <= spp; s += kB) {
         double c[kB][3];
         d2 v[kB];
-        bool dark = true;
+        uint64_t bits = 0;  // OR of the batch's photon bits: 0 iff all four are {+0, +0}
 #pragma unroll
         for (uint32_t j = 0; j < kB; ++j) {
             // final photon {wavelength, intensity}: one 16-B non-temporal load
             VR_GUARD(s + j, p);
             v[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(staging) + ((uint64_t)(s + j) * npix + p));
-            dark = dark && __double_as_longlong(v[j].x) == 0 && __double_as_longlong(v[j].y) == 0;
+            bits |= (uint64_t)__double_as_longlong(v[j].x) | (uint64_t)__double_as_longlong(v[j].y);
         }
-        if (__builtin_amdgcn_uicmp((uint32_t)dark, 0u, 32 /* eq */) == 0) {
+        // the lanes with some nonzero photon bit, as one 64-bit compare into a lane mask.  (Not a
+        // compare of a zero-extended bool "dark" with 0: hipcc of ROCm 7.2 folded that into the
+        // mask of the dark lanes -- the opposite polarity -- once this loop was split in two, so a
+        // wave with ANY dark lane zeroed every lane's colours; DESIGN.md section 8, "the staging
+        // invariant")
+        if (__builtin_amdgcn_uicmpl(bits, 0ull, 33 /* ne */) == 0) {
             // a missed camera ray's photon {+0, +0} (camera.rs:110-113): every lobe is positive at
             // 0 nm, so its colour is (+0, +0, +0) exactly -- the wave skips the 28 exp when all
             // its photons are such (rows of pixels that see no geometry)
@@ -1337,12 +1291,6 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
 #define VR_LAUNCH(C, R, D, M, W)                                                                      \
     hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a, a.scene.prims, \
                        a.scene.materials, a.scene.bvhs)
-    // the timed launches of scenes with an LDS copy of the tree's top (hot_count > 0) take the HOT
-    // instantiation; counting and record launches read every node from memory (same results)
-#define VR_LAUNCH_HOT(D, M)                                                                                    \
-    hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, D, M, 3, false, kHotNodesMax>), grid, block, 0, s, \
-                       a, a.scene.prims, a.scene.materials, a.scene.bvhs)
-    const bool hot = a.scene.hot_count > 0;
 #ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
@@ -1350,13 +1298,11 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     else if (variant == 1) VR_LAUNCH(false, false, D, M, 1); \
     else if (variant == 2) VR_LAUNCH(false, false, D, M, 2); \
     else if (variant == 4) VR_LAUNCH(false, false, D, M, 4); \
-    else if (hot) VR_LAUNCH_HOT(D, M);                     \
     else VR_LAUNCH(false, false, D, M, 3)
 #else
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
     else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
-    else if (hot) VR_LAUNCH_HOT(D, M);                     \
     else VR_LAUNCH(false, false, D, M, 3)
 #endif
     if (!dark0) {
@@ -1369,7 +1315,6 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
         VR_MODES(true, 3);
     }
 #undef VR_MODES
-#undef VR_LAUNCH_HOT
 #undef VR_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
