@@ -618,6 +618,13 @@ struct CallCtx {
 // Environment overrides exist in tuning builds only (python -m vanrijn_amd.build with VR_TUNING=1,
 // -DVR_TUNING_VARIANTS: tools/variants.py threshold sweeps, tools/cycles.py diagnostics); a default
 // build reads no VR_* variable, so nothing in a user's environment changes rendering or timing.
+// launch defaults (A/B builds may override them at compile time)
+#ifndef VR_COOP_SAMPLES  // launches of at most this many pixel-samples may take the cooperative tail
+#define VR_COOP_SAMPLES (4ull << 20)
+#endif
+#ifndef VR_COOP_BOUNCES  // ... once every live path of a wave has bounced this often
+#define VR_COOP_BOUNCES 0u
+#endif
 static const char* tuning_env(const char* name) {
 #ifdef VR_TUNING_VARIANTS
     return getenv(name);
@@ -1037,6 +1044,18 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.leaf_stall = ls ? (uint32_t)std::max(1, atoi(ls)) : 3u;
     const char* lf = tuning_env("VR_LEAF_FEW");  // tuning hook (0: off)
     a.leaf_few = lf ? (uint32_t)std::max(0, atoi(lf)) : 0u;
+    // the cooperative tail (vr_render.hip coop_step, the COOP instantiations): launches of at most
+    // 4 M pixel-samples (a small frame's time is its longest paths') of scenes with a reflective
+    // material (paths trapped between mirror facets run to the 128-bounce limit: C1,
+    // benches/simple_scene.rs).  Scenes without mirrors never take it: on main.rs's Lambertian scene
+    // the breadth-first walk of short tail paths cost more than it saved.
+    {
+        const uint64_t lsamples = a.tile_width * a.tile_height * (uint64_t)p->spp;
+        a.coop = (lsamples <= VR_COOP_SAMPLES && (s->mats & 2) && s->dark0) ? 2u : 0u;
+        if (const char* co = tuning_env("VR_COOP")) a.coop = (uint32_t)std::min(2, std::max(0, atoi(co)));
+        a.coop_bounces = VR_COOP_BOUNCES;  // ... once every live path of the wave has bounced this often
+        if (const char* cb = tuning_env("VR_COOP_BOUNCES")) a.coop_bounces = (uint32_t)std::max(0, atoi(cb));
+    }
     const char* pr = tuning_env("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {

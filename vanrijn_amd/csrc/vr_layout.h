@@ -145,7 +145,11 @@ struct RenderArgs {
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     uint32_t leaf_few;            // ... or at most this many lanes are still traversing
-    uint32_t pad_args;
+    // the launch's tail (COOP instantiations): a wave's last 1 or 2 paths walk their trees with the
+    // wave's lanes once each has bounced `coop_bounces` times; coop = owners served (0: off)
+    uint32_t coop;
+    uint32_t coop_bounces;
+    uint32_t pad_coop;
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)

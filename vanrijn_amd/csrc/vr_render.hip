@@ -141,7 +141,10 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
-template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false>
+// COOP: the cooperative tail (coop_step below) -- instantiated for the small launches of scenes with
+// a reflective material, the only ones whose time is a few trapped paths (vr_host.cpp make_args).
+template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
+          bool COOP = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -158,6 +161,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     __shared__ uint8_t wl_own[4 * kWaveList];
     __shared__ unsigned long long lr_d[256], lr_key[256];  // key: rank << 32 | triangle
     __shared__ uint32_t lr_cnt[256];
+    // COOP: an owner's stack column map (coop_step)
+    __shared__ uint32_t coop_map[COOP ? 256 : 1];
     const int wbase = (threadIdx.x >> 6) * kWaveList;
     uint32_t q_head = 0, q_tail = 0;  // wave-uniform FIFO positions (mod kWaveList)
     const int tid = threadIdx.x;
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     lr_d[tid] = ~0ull;  // each lane's result slot is only touched by its own wave
     lr_key[tid] = 0;
     lr_cnt[tid] = 0;
+    if (COOP) coop_map[tid] = 0;
     DeviceScene S = A.scene;
     S.prims = g_prims;
     S.materials = g_materials;
@@ -200,6 +206,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     uint32_t px = 0, py = 0, s_end = 0;
     int state = kNeedRay;  // with s_idx == s_end: needs a work item
     uint32_t s_idx = 0;
+    bool coop_on = false;  // COOP: this wave's tail walks its last paths cooperatively (sticky)
     uint64_t w_next = 0, w_end = 0;  // this wave's slice of the queue (grab > 0)
     Rng rng;
     rng.reset(0);
@@ -635,6 +642,149 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         state = kRayReady;
     };
 
+    // The launch's tail (COOP instantiations): the queue is exhausted and one or two paths are left
+    // in the wave -- in a small frame of a scene with mirrors, paths trapped between facets run to
+    // the 128-bounce recursion limit and set the frame's time (C1, benches/simple_scene.rs: 25 of
+    // its 3,072 waves hold one or two and end at 3.5-6.4 ms, the others by 1.1 ms).  Their walks are
+    // spread over the wave's lanes: with one owner every lane works for it, with two the lower half
+    // of the lanes works for the lower owner and the upper half for the other.  Each step takes the
+    // owner's current node and up to (workers - 1) entries from the top of its stack, one per worker,
+    // tests them against the owner's ray, pushes the hit interior children back and queues the hit
+    // leaves for the owner.  An owner's stack spans extra lane columns of the wave (the other lanes
+    // are done): with one owner from the start, the next columns in turn; once two owners have shared
+    // the wave (coop_map, sticky for the rest of the launch), each owner keeps its own column plus the
+    // lanes of its half other than the two owners', so the map never changes under an owner whose
+    // partner finishes first.  Culling and the order-independent leaf rounds keep the closest hit and
+    // its tie rule: only the visiting order changes.  Called with the whole wave
+    // active; `live` holds the one or two live lanes.
+    // the LDS word of virtual stack entry v of owner o whose column map is om (coop_map)
+    auto coop_vaddr = [&](int o, uint32_t om, int v) {
+        const int j = v / STACK, og = (int)(om & 3) - 1, op = (int)(om >> 8);
+        int col;
+        if (j == 0) {
+            col = o;
+        } else if (og < 0) {
+            col = (o + j) & 63;
+        } else {  // the (j-1)-th lane of half og that is neither owner
+            const int s1 = o < op ? o : op, s2 = o < op ? op : o, lo = og * 32;
+            col = lo + j - 1;
+            if (s1 >= lo && s1 < lo + 32 && col >= s1) ++col;
+            if (s2 >= lo && s2 < lo + 32 && col >= s2) ++col;
+        }
+        return (v % STACK) * 256 + (tid & ~63) + col;
+    };
+    auto coop_step = [&](const uint64_t live) {
+        uint32_t lmask = 0;
+        int32_t lent[4];
+        const int oa = (int)__builtin_ctzll(live);         // lower owner
+        const int ob = (int)(63 - __builtin_clzll(live));  // upper owner (== oa: one owner)
+        const bool two = oa != ob;
+        uint32_t* cmap = &coop_map[tid & ~63];  // per lane: 0 (full map), or 1 + half | partner << 8
+        if (two && cmap[oa] == 0) {
+            if ((int)lane == oa) cmap[oa] = 1u | ((uint32_t)ob << 8);
+            if ((int)lane == ob) cmap[ob] = 2u | ((uint32_t)oa << 8);
+        }
+        // this lane works for its half's owner (two owners) or the one owner
+        const bool upper = two && lane >= 32;
+        const int owner = upper ? ob : oa;
+        const int gbase = upper ? 32 : 0, gsize = two ? 32 : 64;
+        const uint64_t gmask = two ? (upper ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
+        const int r = (int)lane - gbase;  // worker rank
+        const uint32_t om = cmap[owner];  // the owner's column map
+        const int o_sp = __shfl(sp, owner);
+        const int o_node = __shfl(node, owner);
+        const bool o_trav = __shfl(state == kTraversing ? 1 : 0, owner) != 0;
+        const int have = o_trav ? (o_node >= 0 ? 1 : 0) + o_sp : 0;
+        // the owner's stack capacity: every column of the wave, or its own plus 30 of its half
+        const int cap = ((om & 3) == 0 ? 64 : 31) * STACK;
+        // entries taken this step: at most one per worker, and at most what keeps 150 entries of
+        // headroom (a step adds at most 3 net per entry taken; a depth-first walk from a near-full
+        // stack needs at most 3 per level below)
+        int t = have < gsize ? have : gsize;
+        const int room = (cap - 150 - have) / 3;
+        if (t > room) t = room < 1 ? (have > 0 ? 1 : 0) : room;
+        const bool work = t > 0 && VR_ROOM;  // uniform per half
+        uint32_t im = 0;                     // hit interior children
+        int c[4] = {0, 0, 0, 0};
+        int pos = o_sp;
+        if (work) {
+            VR_MARK("coop_step");
+            const int first_stack = o_node >= 0 ? 1 : 0;  // worker 0 takes the current node
+            int my = -1;
+            if (r < t) my = (r < first_stack) ? o_node : (int)st_node[coop_vaddr(owner, om, o_sp - 1 - (r - first_stack))];
+            pos = o_sp - (t - first_stack);  // stack entries left below the taken ones
+            Ray32 ry;                        // the owner's ray and cull bounds
+            ry.ox = __shfl(pre32.ox, owner);
+            ry.oy = __shfl(pre32.oy, owner);
+            ry.oz = __shfl(pre32.oz, owner);
+            ry.ix = __shfl(pre32.ix, owner);
+            ry.iy = __shfl(pre32.iy, owner);
+            ry.iz = __shfl(pre32.iz, owner);
+            ry.nx = __shfl(pre32.nx, owner);
+            ry.ny = __shfl(pre32.ny, owner);
+            ry.nz = __shfl(pre32.nz, owner);
+            ry.ek = __shfl(pre32.ek, owner);
+            const float cf = __shfl(cull_far, owner);
+            const float cb = __shfl(cull_behind, owner);
+            if (my >= 0) {
+                const Node4& nd = VR_NODES4[my];
+                if (COUNT) cnt.node_visits++;
+                uint32_t xm = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    c[k] = nd.child[k];
+                    float f, g;
+                    bool maybe, sure;
+                    slab32_flags(nd.box[k], ry, f, g, maybe, sure);
+                    const bool lv = c[k] != kEmptyChild;
+                    if (COUNT && lv) cnt.box_tests++;
+                    const bool pass = lv && maybe && !(f > cf || g < cb);
+                    xm |= (pass && !sure) ? 1u << k : 0u;
+                    im |= (pass && c[k] >= 0) ? 1u << k : 0u;
+                    lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
+                    lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
+                }
+            }
+        }
+        // interior hits onto the owner's stack, in (child slot, worker) order
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool ih = (im >> k) & 1u;
+            const uint64_t m = __ballot(ih) & gmask;
+            if (ih) st_node[coop_vaddr(owner, om, pos + (int)lanes_below(m))] = (uint32_t)c[k];
+            pos += (int)__popcll(m);
+        }
+        // each owner takes its next node, the top of its stack: its workers' pos and work flag
+        // (uniform over its half) by permute from the half's first lane
+        const int lead = (two && (int)lane == ob) ? 32 : 0;
+        const int npos = __shfl(pos, lead);
+        const bool nwork = __shfl(work ? 1 : 0, lead) != 0;
+        const bool is_owner = ((live >> lane) & 1ull) != 0;
+        if (is_owner && nwork) {
+            sp = npos;
+            if (sp > 0) {
+                --sp;
+                node = (int)st_node[coop_vaddr((int)lane, cmap[lane], sp)];
+            } else {
+                node = -1;
+            }
+        }
+        // the hit leaves, queued for their owners in (child slot, lane) order
+        const uint64_t own_mask = two ? ((int)lane == ob ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool lh = (lmask >> k) & 1u;
+            const uint64_t m = __ballot(lh);
+            if (lh) {
+                const uint32_t qp = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
+                wl_tri[wbase + qp] = lent[k];
+                wl_own[wbase + qp] = (uint8_t)owner;
+            }
+            q_tail += (uint32_t)__popcll(m);
+            if (is_owner) np += (int)__popcll(m & own_mask);
+        }
+        q_tail = __builtin_amdgcn_readfirstlane(q_tail);
+    };
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
@@ -813,11 +963,27 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // node step (4-wide node), while the wave FIFO has room for four more leaves per lane
             uint32_t lmask = 0;  // leaf children this lane queues in this step
             int32_t lent[4];
+            bool coop = false;
+            if constexpr (COOP) {
+                if (A.coop && tail) {  // some lane of the wave is done: the queue is exhausted
+                    const uint64_t live = __ballot(state != kDone);
+                    const int nlive = __popcll(live);
+                    // A.coop: owners served (1 or 2); to start, every live path must have bounced
+                    // A.coop_bounces times.  Once on, it stays on for the wave: an owner's stack may
+                    // span other lanes' columns, and the live set only shrinks (a live lane may still
+                    // start a new path from the wave's slice, with its own empty stack)
+                    if (!coop_on)
+                        coop_on = nlive >= 1 && nlive <= (int)A.coop &&
+                                  (__ballot(state != kDone && bounces >= (int)A.coop_bounces) == live);
+                    coop = coop_on && nlive >= 1;
+                    if (coop) coop_step(live);
+                }
+            }
             if (COUNT) {  // how full this iteration's node step is (the headroom of merging waves)
                 const int n = VR_ROOM ? __popcll(lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) : 0;
                 if (first_active_lane()) step_hist[n == 0 ? 0 : 1 + (n - 1) / 8]++;
             }
-            if (state == kTraversing && node >= 0 && VR_ROOM) {
+            if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
                 const Node4& nd = VR_NODES4[node];
                 if (COUNT) cnt.node_visits++;
@@ -919,7 +1085,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const bool room = VR_ROOM;  // wave-uniform
                 const uint64_t at_node = trav & lanes_ige(node, 0);
                 const uint64_t stalled_m = lanes_igt(np, 0) & (room ? ~lanes_ige(node, 0) : exec_mask());
-                const bool few = tail && __popcll(trav) <= (int)A.leaf_few;
+                const bool few = coop || (tail && __popcll(trav) <= (int)A.leaf_few);
                 if (queued >= A.leaf_threshold || few || __popcll(stalled_m) >= (int)A.leaf_stall ||
                     !room || at_node == 0) {
                     VR_SEC(0);
@@ -1291,6 +1457,11 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
 #define VR_LAUNCH(C, R, D, M, W)                                                                      \
     hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a, a.scene.prims, \
                        a.scene.materials, a.scene.bvhs)
+    // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
+    // of scenes with a reflective material)
+#define VR_LAUNCH_COOP(D, M)                                                                                 \
+    hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, D, M, 3, false, true>), grid, block, 0, s, a, \
+                       a.scene.prims, a.scene.materials, a.scene.bvhs)
 #ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
 #define VR_MODES(D, M)                                     \
     if (recording) VR_LAUNCH(false, true, D, M, 3);        \
@@ -1305,16 +1476,20 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
     else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
     else VR_LAUNCH(false, false, D, M, 3)
 #endif
+    const bool coop = a.coop != 0 && !recording && !counting;
     if (!dark0) {
         VR_MODES(false, 3);
     } else if (mats == 1) {
         VR_MODES(true, 1);
     } else if (mats == 2) {
-        VR_MODES(true, 2);
+        if (coop) VR_LAUNCH_COOP(true, 2);
+        else VR_MODES(true, 2);
     } else {
-        VR_MODES(true, 3);
+        if (coop) VR_LAUNCH_COOP(true, 3);
+        else VR_MODES(true, 3);
     }
 #undef VR_MODES
+#undef VR_LAUNCH_COOP
 #undef VR_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
