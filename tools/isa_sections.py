@@ -14,9 +14,10 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the C3 timed kernel: STACK 32, Lambertian-only, DARK0, the LDS tree top (HOT = 32; VR_ISA_HOT=0: without)
-KERNEL = ("_ZN2vr3dev13render_kernelILi32ELb0ELb0ELb1ELi1ELi3ELb0ELi%sEEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
-          % os.environ.get("VR_ISA_HOT", "32"))
+# the C3 timed kernel: STACK 32, Lambertian-only, DARK0, no Whitted, no cooperative tail (VR_ISA_STACK /
+# VR_ISA_MATS / VR_ISA_COOP=1 pick another instantiation)
+KERNEL = ("_ZN2vr3dev13render_kernelILi%sELb0ELb0ELb1ELi%sELi3ELb0ELb%sEEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
+          % (os.environ.get("VR_ISA_STACK", "32"), os.environ.get("VR_ISA_MATS", "1"), os.environ.get("VR_ISA_COOP", "0")))
 
 
 def cost(op):
@@ -41,6 +42,7 @@ def main():
     start = next(i for i, l in enumerate(lines) if l.startswith(KERNEL + ":"))
     sec = "entry"
     stats = collections.defaultdict(lambda: collections.Counter())
+    ops = collections.defaultdict(lambda: collections.Counter())
     for l in lines[start + 1:]:
         if l.startswith(".Lfunc_end"):
             break
@@ -54,6 +56,7 @@ def main():
         op = t.split()[0]
         st = stats[sec]
         st["insts"] += 1
+        ops[sec][op] += 1
         if op.startswith("v_"):
             st["valu"] += 1
             st["cycles"] += cost(op)
@@ -69,6 +72,9 @@ def main():
     for k, st in stats.items():
         print("%-14s %6d %6d %6d %6d %7d %5d %5d" % (k, st["insts"], st["valu"], st["f64"], st["salu"], st["cycles"],
                                                     st["vmem"], st["lds"]))
+    for k in os.environ.get("VR_ISA_OPS", "").split(","):  # opcode histograms of these sections
+        if k in ops:
+            print("\n" + k + ": " + ", ".join("%s %d" % kv for kv in ops[k].most_common() if kv[0].startswith("v_")))
 
 
 if __name__ == "__main__":
