@@ -1056,6 +1056,13 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         a.coop_bounces = VR_COOP_BOUNCES;  // ... once every live path of the wave has bounced this often
         if (const char* cb = tuning_env("VR_COOP_BOUNCES")) a.coop_bounces = (uint32_t)std::max(0, atoi(cb));
     }
+    {
+        // the node step's child keys keep the entry distance's high bits above the node index:
+        // the fewest low bits whose all-ones value exceeds every wide node index
+        uint32_t m = 1;
+        while (m < s->wide_count + 1 && m != 0xffffffffu) m = m << 1 | 1;
+        a.sort_mask = m;
+    }
     const char* pr = tuning_env("VR_PHASE_A_REPS");  // tuning hook
     a.phase_a_reps = pr ? (uint32_t)std::max(1, atoi(pr)) : 2u;
     {

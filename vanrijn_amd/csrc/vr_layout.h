@@ -149,7 +149,7 @@ struct RenderArgs {
     // wave's lanes once each has bounced `coop_bounces` times; coop = owners served (0: off)
     uint32_t coop;
     uint32_t coop_bounces;
-    uint32_t pad_coop;
+    uint32_t sort_mask;           // node step's packed child keys: low bits = child index (2^k - 1 > every wide node index)
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)

@@ -961,7 +961,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             VR_MARK("phaseB_top");
             __builtin_amdgcn_s_setprio(kPrioNode);
             // node step (4-wide node), while the wave FIFO has room for four more leaves per lane
-            uint32_t lmask = 0;  // leaf children this lane queues in this step
+            bool lq[4] = {false, false, false, false};  // leaf children this lane queues in this step
             int32_t lent[4];
             bool coop = false;
             if constexpr (COOP) {
@@ -1010,43 +1010,52 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
                 // leaf children: their triangles go to the wave FIFO, appended after the step by all
                 // lanes at once
-                float key[4];
-                int ch[4];
+                // interior children near-first: one 32-bit key per child, the entry distance's high
+                // bits (clamped below at 0: non-negative f32 bits order like the values) over the
+                // child's node index (A.sort_mask: the low bits, wide enough for every wide node), so
+                // the sorting network is integer min / max and the index rides along; 0xffffffff
+                // (or any key with bit 31 set) marks "not descended".  Only the visiting order depends on the key.
+                const uint32_t smask = A.sort_mask;
+                uint32_t key[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const bool h = (hm >> k) & 1u;
                     lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
-                    lmask |= (h && c[k] < 0) ? 1u << k : 0u;
-                    // hit: a finite key (NaN or infinite f32 bounds of exactly-decided children
-                    // clamp into range); INFINITY marks "not descended"
-                    key[k] = (h && c[k] >= 0) ? fminf(fmaxf(f[k], -FLT_MAX), FLT_MAX) : INFINITY;
-                    ch[k] = c[k];
+                    lq[k] = h && c[k] < 0;
+                    // a leaf or empty child's index is negative: its key has bit 31 set as it is
+                    // (negative distances, -0 and negative NaNs clamp to 0 as integers; +inf and
+                    // positive NaNs keep bit 31 clear: a hit child is never dropped)
+                    uint32_t kb = ((uint32_t)max(__float_as_int(f[k]), 0) & ~smask) | (uint32_t)c[k];
+                    asm volatile("" : "+v"(kb));  // computed for every lane: a select, not a branch
+                    key[k] = h ? kb : 0xffffffffu;
                 }
-                // interior children near-first: sorting network on (entry distance, child)
                 auto cas = [&](int i, int j) {
-                    const bool sw = key[j] < key[i];
-                    const float ki = key[i], kj = key[j];
-                    const int ci = ch[i], cj = ch[j];
-                    key[i] = sw ? kj : ki;
-                    key[j] = sw ? ki : kj;
-                    ch[i] = sw ? cj : ci;
-                    ch[j] = sw ? ci : cj;
+                    const uint32_t ki = key[i], kj = key[j];
+                    key[i] = ki < kj ? ki : kj;
+                    key[j] = ki < kj ? kj : ki;
                 };
                 cas(0, 1);
                 cas(2, 3);
                 cas(0, 2);
                 cas(1, 3);
                 cas(1, 2);
-                if (key[0] < INFINITY) {
+                if (key[0] < 0x80000000u) {
                     // farthest first, so the nearest remaining pops first (writes at sp are
                     // unconditional: the stack holds one spare entry)
-                    st_node[sp * 256 + tid] = (uint32_t)ch[3];
-                    sp += key[3] < INFINITY ? 1 : 0;
-                    st_node[sp * 256 + tid] = (uint32_t)ch[2];
-                    sp += key[2] < INFINITY ? 1 : 0;
-                    st_node[sp * 256 + tid] = (uint32_t)ch[1];
-                    sp += key[1] < INFINITY ? 1 : 0;
-                    node = ch[0];
+                    // (sp advances by 1 + (key >> 31 arithmetic): 1 for a descended child, 0 else)
+                    int32_t adv[4];
+#pragma unroll
+                    for (int k = 1; k < 4; ++k) {
+                        adv[k] = (int32_t)key[k] >> 31;
+                        asm volatile("" : "+v"(adv[k]));  // keeps the shift: LLVM would rebuild it as not + shift
+                    }
+                    st_node[sp * 256 + tid] = key[3] & smask;
+                    sp += 1 + adv[3];
+                    st_node[sp * 256 + tid] = key[2] & smask;
+                    sp += 1 + adv[2];
+                    st_node[sp * 256 + tid] = key[1] & smask;
+                    sp += 1 + adv[1];
+                    node = (int)(key[0] & smask);
                 } else if (sp > 0) {
                     --sp;
                     node = (int)st_node[sp * 256 + tid];
@@ -1059,11 +1068,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             __builtin_amdgcn_s_setprio(kPrioLeaf);
             // append this step's leaves to the wave FIFO in (child slot, lane) order (skipped when no
             // lane met a leaf: main -1.3 %, C5 -4.5 %)
-            if (lanes_ine((int)lmask, 0))
+            if ((__ballot(lq[0]) | __ballot(lq[1]) | __ballot(lq[2]) | __ballot(lq[3])) != 0)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const bool lh = (lmask >> k) & 1u;
-                const uint64_t m = lanes_ine((int)(lmask & (1u << k)), 0);
+                const bool lh = lq[k];
+                const uint64_t m = __ballot(lh);
                 if (lh) {
                     const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
                     wl_tri[wbase + pos] = lent[k];
