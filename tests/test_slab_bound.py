@@ -6,7 +6,9 @@ max|i32|; it answers "hit" only if hi - lo > 2E, "miss" only if lo - hi > 2E, an
 the reference's f64 division test (raycasting/axis_aligned_bounding_box.rs:9-27).  Here the f32
 arithmetic is emulated exactly (numpy float32 operations are IEEE round-to-nearest; the fma is
 formed in float64 from exact float32 products and rounded once) on rays and boxes built to sit on
-or near a tie, and every f32 verdict must equal the f64 division verdict.
+or near a tie, and every f32 verdict must equal the f64 division verdict.  The kernel's reciprocals
+are the hardware's v_rcp_f32 (within 1 ulp of 1/d, not correctly rounded): the test also takes,
+per axis at random, either f32 neighbour of the exact reciprocal.
 """
 import numpy as np
 
@@ -43,10 +45,28 @@ def fma32(a, b, c):
                                                                # is below the bound's slack)
 
 
-def f32_slab(b32, o, d, extent):
-    o32 = o.astype(F32)
+def recip32(d32, rng=None):
+    """1 / d32 correctly rounded, or (rng given) either f32 neighbour of the exact value: what a
+    1-ulp reciprocal may return"""
     with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
-        i32 = (F32(1.0) / d.astype(F32)).astype(F32)
+        rn = (F32(1.0) / d32).astype(F32)
+        if rng is None:
+            return rn
+        out = rn.copy()
+        for a in range(3):
+            exact = 1.0 / np.float64(d32[a]) if d32[a] != 0 else np.inf
+            if not np.isfinite(exact) or not np.isfinite(rn[a]):
+                continue
+            down = rn[a] if float(rn[a]) <= exact else np.nextafter(rn[a], F32(-np.inf))
+            up = rn[a] if float(rn[a]) >= exact else np.nextafter(rn[a], F32(np.inf))
+            out[a] = down if rng.random() < 0.5 else up
+        return out
+
+
+def f32_slab(b32, o, d, extent, rcp_rng=None):
+    o32 = o.astype(F32)
+    i32 = recip32(d.astype(F32), rcp_rng)
+    with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
         n32 = -(o32 * i32)
     big = max(extent, float(np.abs(o).max())) + 1.0
     ek = 6e-7 * big * float(np.abs(i32).max())
@@ -62,8 +82,13 @@ def f32_slab(b32, o, d, extent):
     return 2
 
 
-def test_f32_pretest_never_contradicts_the_exact_test():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("rcp", ["rn", "1ulp"])
+def test_f32_pretest_never_contradicts_the_exact_test(rcp):
     rng = np.random.default_rng(5)
+    rcp_rng = np.random.default_rng(11) if rcp == "1ulp" else None
     extent = 8.0
     decided = undecided = 0
     for _ in range(20000):
@@ -84,7 +109,7 @@ def test_f32_pretest_never_contradicts_the_exact_test():
         b = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]])
         b = np.clip(b, -extent, extent)
         b[1::2] = np.maximum(b[1::2], b[0::2])
-        r = f32_slab(outward(b), o, d, extent)
+        r = f32_slab(outward(b), o, d, extent, rcp_rng)
         exact = f64_slab(b, o, d)
         if r == 2:
             undecided += 1

@@ -366,8 +366,13 @@ struct Ray32 {
 __device__ __forceinline__ Ray32 prepare32(const RayPre& p, double extent) {
     Ray32 r;
     r.ox = (float)p.o.x; r.oy = (float)p.o.y; r.oz = (float)p.o.z;
-    // correctly rounded f32 reciprocals of the f32 direction: within 1.2e-7 relative of 1/d
-    r.ix = 1.0f / (float)p.d.x; r.iy = 1.0f / (float)p.d.y; r.iz = 1.0f / (float)p.d.z;
+    // hardware f32 reciprocals of the f32 direction (v_rcp_f32: within 1 ulp, 1.2e-7 relative, of
+    // 1/d -- the bound's reciprocal term; tests/test_slab_bound.py takes either f32 neighbour of the
+    // exact value).  |d| = 1, so some |1/d_i| >= 1 and no reciprocal is denormal; a denormal or
+    // zero d_i gives an infinite or huge reciprocal, ek = +inf, and every test takes the f64 path
+    r.ix = __builtin_amdgcn_rcpf((float)p.d.x);
+    r.iy = __builtin_amdgcn_rcpf((float)p.d.y);
+    r.iz = __builtin_amdgcn_rcpf((float)p.d.z);
     r.nx = -(r.ox * r.ix); r.ny = -(r.oy * r.iy); r.nz = -(r.oz * r.iz);
     // origins on the infinite plane can lie outside the scene extent: bound with |o| too
     const double big = fmax(extent, fmax(fmax(fabs(p.o.x), fabs(p.o.y)), fabs(p.o.z))) + 1.0;

@@ -1068,11 +1068,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             __builtin_amdgcn_s_setprio(kPrioLeaf);
             // append this step's leaves to the wave FIFO in (child slot, lane) order (skipped when no
             // lane met a leaf: main -1.3 %, C5 -4.5 %)
-            if ((__ballot(lq[0]) | __ballot(lq[1]) | __ballot(lq[2]) | __ballot(lq[3])) != 0)
+            const uint64_t lqm[4] = {__ballot(lq[0]), __ballot(lq[1]), __ballot(lq[2]), __ballot(lq[3])};
+            if ((lqm[0] | lqm[1] | lqm[2] | lqm[3]) != 0)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool lh = lq[k];
-                const uint64_t m = __ballot(lh);
+                const uint64_t m = lqm[k];
                 if (lh) {
                     const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
                     wl_tri[wbase + pos] = lent[k];
