@@ -2,7 +2,9 @@
 
 The kernel decides most box tests in f32: slab values t = fma(b32, i32, -(o32 * i32)) on the
 outward-rounded box, error margin E = ek + 3e-7 (|lo| + |hi|), ek = 6e-7 (max(extent, |o|) + 1)
-max|i32|; it answers "hit" only if hi - lo > 2E, "miss" only if lo - hi > 2E, and otherwise re-runs
+max|i32| (since round 4 the kernel uses the per-ray constant E = 3.001 ek, which bounds that margin
+for every box within the scene extent: checked case by case here); it answers "hit" only if
+hi - lo > 2E, "miss" only if lo - hi > 2E, and otherwise re-runs
 the reference's f64 division test (raycasting/axis_aligned_bounding_box.rs:9-27).  Here the f32
 arithmetic is emulated exactly (numpy float32 operations are IEEE round-to-nearest; the fma is
 formed in float64 from exact float32 products and rounded once) on rays and boxes built to sit on
@@ -63,7 +65,7 @@ def recip32(d32, rng=None):
         return out
 
 
-def f32_slab(b32, o, d, extent, rcp_rng=None):
+def f32_slab(b32, o, d, extent, rcp_rng=None, const_margin=False):
     o32 = o.astype(F32)
     i32 = recip32(d.astype(F32), rcp_rng)
     with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
@@ -75,6 +77,20 @@ def f32_slab(b32, o, d, extent, rcp_rng=None):
     lo = max(min(t[0], t[1]), min(t[2], t[3]), min(t[4], t[5]))
     hi = min(max(t[0], t[1]), max(t[2], t[3]), max(t[4], t[5]))
     e = F32(ek + F32(3e-7) * (abs(lo) + abs(hi)))
+    if const_margin:
+        # the kernel's form since round 4: E = 3.001 ek per ray (vr_device.h Ray32), which bounds the
+        # per-box margin above for every box of the scene; one difference, two compares
+        e2 = 2.0 * (3.001 * (6e-7 * big * float(np.abs(i32).max())))
+        # round_away_f32: (float)t times 1 + 2^-22, rounded (at least t)
+        E2 = F32(F32(e2) * F32(1.0 + 2.0 ** -22)) if e2 < 1e30 else F32(np.inf)
+        assert float(E2) >= e2
+        assert float(E2) >= 2.0 * float(e), (float(E2), float(e))
+        dd = F32(lo - hi)
+        if dd < -E2:
+            return 1
+        if dd > E2:
+            return 0
+        return 2
     if F32(hi - lo) > F32(2.0) * e:
         return 1
     if F32(lo - hi) > F32(2.0) * e:
@@ -85,8 +101,9 @@ def f32_slab(b32, o, d, extent, rcp_rng=None):
 import pytest  # noqa: E402
 
 
+@pytest.mark.parametrize("const_margin", [False, True])
 @pytest.mark.parametrize("rcp", ["rn", "1ulp"])
-def test_f32_pretest_never_contradicts_the_exact_test(rcp):
+def test_f32_pretest_never_contradicts_the_exact_test(rcp, const_margin):
     rng = np.random.default_rng(5)
     rcp_rng = np.random.default_rng(11) if rcp == "1ulp" else None
     extent = 8.0
@@ -109,7 +126,7 @@ def test_f32_pretest_never_contradicts_the_exact_test(rcp):
         b = np.array([lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]])
         b = np.clip(b, -extent, extent)
         b[1::2] = np.maximum(b[1::2], b[0::2])
-        r = f32_slab(outward(b), o, d, extent, rcp_rng)
+        r = f32_slab(outward(b), o, d, extent, rcp_rng, const_margin)
         exact = f64_slab(b, o, d)
         if r == 2:
             undecided += 1

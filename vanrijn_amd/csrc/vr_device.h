@@ -361,8 +361,21 @@ __device__ __forceinline__ bool slab(const double* b, const RayPre& p, double& t
 struct Ray32 {
     float ox, oy, oz, ix, iy, iz;
     float nx, ny, nz;  // -(o * inv) per axis (f32): slab values are fma(bound, inv, n)
-    float ek;  // 6e-7 * X * max_i |1/d_i| (+inf: every test falls back to f64)
+    float e2;  // 2 E, E = 3.001 ek >= every box's ek + 3e-7 (|lo| + |hi|) (+inf: every test falls back to f64)
 };
+// The margin as one per-ray constant (round 4).  The bound per box was E_box = ek + 3e-7 (|lo| + |hi|)
+// with ek = 6e-7 X m (X = max(extent, |o|) + 1, m = max_i |1/d_i|).  Every slab value is
+// fma(b, i, -(o i)) with |b| <= extent (the scene's coordinates bound every box, rounded outward by
+// at most 2^-23 relative) and |o| <= X - 1, so |t| <= 2 X m (1 + 2^-22); lo and hi are slab values,
+// hence 3e-7 (|lo| + |hi|) <= 1.2e-6 X m (1 + 2^-22) = 2 ek (1 + 2^-22), and E_box (its f32 evaluation
+// included) < 3.001 ek = E.  A decision taken with E is taken with E_box too, so it inherits that
+// bound's soundness (tests/test_slab_bound.py checks both); it saves the per-box margin arithmetic
+// (|lo| + |hi|, the fma, lo - e, hi + e, 2e) in the node step, and the cull thresholds carry E.
+// an f32 at least as far from 0 as t (a normal or infinite t): (float)t is within 2^-24 relative of t,
+// and one product by 1 + 2^-22 (rounded) moves it beyond -- one multiply instead of a compare and
+// nextafterf.  Used for the cull thresholds (t >= margin > 0 away from +0, or t <= -behind_margin)
+// and the margin itself, where a wider value is only more conservative.
+__device__ __forceinline__ float round_away_f32(double t) { return (float)t * (1.0f + 0x1p-22f); }
 __device__ __forceinline__ Ray32 prepare32(const RayPre& p, double extent) {
     Ray32 r;
     r.ox = (float)p.o.x; r.oy = (float)p.o.y; r.oz = (float)p.o.z;
@@ -378,48 +391,46 @@ __device__ __forceinline__ Ray32 prepare32(const RayPre& p, double extent) {
     const double big = fmax(extent, fmax(fmax(fabs(p.o.x), fabs(p.o.y)), fabs(p.o.z))) + 1.0;
     const double m = fmax(fmax(fabsf(r.ix), fabsf(r.iy)), fabsf(r.iz));
     const double ek = 6e-7 * big * m;
-    r.ek = (p.exact_only() || !(ek < 1e30)) ? INFINITY : (float)ek;
+    r.e2 = (p.exact_only() || !(ek < 1e30)) ? INFINITY : round_away_f32(2.0 * (3.001 * ek));
     return r;
 }
+// E (half of e2; exact), for the cull thresholds
+__device__ __forceinline__ double margin_of(const Ray32& r) { return 0.5 * (double)r.e2; }
 // Each slab value is one fused multiply-add per bound, two bounds per packed (v_pk_fma_f32)
 // instruction: t = RN(b32 * i32 - RN(o32 * i32)).  Its error against the exact (b - o) / d is at
 // most 1.8e-7 |t| + 2.4e-7 X |1/d| (reciprocal of the f32 direction 1.2e-7, fma 6e-8;
 // outward-rounded bound 2^-23 |b|, f32 origin and the product o * i 2^-24 each), which
-// E = ek + 3e-7 (|lo| + |hi|) covers (ek = 6e-7 X max |1/d|).
+// E_box = ek + 3e-7 (|lo| + |hi|) covers (ek = 6e-7 X max |1/d|); the per-ray E >= E_box (above).
+// lo / hi are returned as computed: the exact interval lies within [lo - E, hi + E], and the cull
+// thresholds the callers compare them with are widened by E (cull_far + E rounded up, cull_behind -
+// E rounded down), so `lo > cull_far'` implies lo - E > cull_far.
 typedef float vr_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& tlo, float& thi) {
+__device__ __forceinline__ int slab32(const float* b, const Ray32& r, float& lo, float& hi) {
     const vr_f2 bx = {b[0], b[1]}, by = {b[2], b[3]}, bz = {b[4], b[5]};
     const vr_f2 tx = __builtin_elementwise_fma(bx, (vr_f2){r.ix, r.ix}, (vr_f2){r.nx, r.nx});
     const vr_f2 ty = __builtin_elementwise_fma(by, (vr_f2){r.iy, r.iy}, (vr_f2){r.ny, r.ny});
     const vr_f2 tz = __builtin_elementwise_fma(bz, (vr_f2){r.iz, r.iz}, (vr_f2){r.nz, r.nz});
-    const float lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-    const float hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const float e = r.ek + 3e-7f * (fabsf(lo) + fabsf(hi));
-    tlo = lo - e;
-    thi = hi + e;
-    if (hi - lo > 2.0f * e) return 1;
-    if (lo - hi > 2.0f * e) return 0;
+    lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    // lo - hi is exactly -(hi - lo) (round to nearest): both tests on one difference; NaN: 2
+    const float d = lo - hi;
+    if (d < -r.e2) return 1;
+    if (d > r.e2) return 0;
     return 2;
 }
 // slab32 as two flags (the node step's form, no integer result to re-test): `maybe` = the exact
-// test may pass (slab32 != 0), `sure` = it certainly passes (slab32 == 1)
-__device__ __forceinline__ void slab32_flags(const float* b, const Ray32& r, float& tlo, float& thi, bool& maybe,
+// test may pass (slab32 != 0; also for a NaN difference), `sure` = it certainly passes (slab32 == 1)
+__device__ __forceinline__ void slab32_flags(const float* b, const Ray32& r, float& lo, float& hi, bool& maybe,
                                              bool& sure) {
     const vr_f2 bx = {b[0], b[1]}, by = {b[2], b[3]}, bz = {b[4], b[5]};
     const vr_f2 tx = __builtin_elementwise_fma(bx, (vr_f2){r.ix, r.ix}, (vr_f2){r.nx, r.nx});
     const vr_f2 ty = __builtin_elementwise_fma(by, (vr_f2){r.iy, r.iy}, (vr_f2){r.ny, r.ny});
     const vr_f2 tz = __builtin_elementwise_fma(bz, (vr_f2){r.iz, r.iz}, (vr_f2){r.nz, r.nz});
-    const float lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-    const float hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const float e = r.ek + 3e-7f * (fabsf(lo) + fabsf(hi));
-    tlo = lo - e;
-    thi = hi + e;
-    // slab32's two tests on one difference: lo - hi is exactly -(hi - lo) (round to nearest), so
-    // !(lo - hi > 2e) is !(hi - lo < -2e) -- also true for a NaN difference -- and it holds
-    // whenever `sure` does (e >= 0)
-    const float d = hi - lo, e2 = 2.0f * e;
-    sure = d > e2;
-    maybe = !(d < -e2);
+    lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    const float d = lo - hi;
+    sure = d < -r.e2;
+    maybe = !(d > r.e2);
 }
 
 // A triangle record in one batch of five dwordx4 loads.  Left to itself the scheduler issued the
@@ -634,6 +645,7 @@ struct Best {
     int kind;
     int index;   // prim index, or global leaf-ordered triangle index
     int object;  // scene object index (ties between objects: the earlier object wins, min_by)
+    uint32_t rank;  // a triangle's reference rank (TriVerts::rank; ties within a BVH: the higher wins)
     double bary[3];
 };
 
@@ -666,15 +678,15 @@ __device__ __forceinline__ void traverse_bvh(const DeviceScene& S, const Bvh& bv
         double b[3];
         double d = triangle_distance(S.tris[tri], p, b);
         if (d < 0.0) return;
-        bool take;
-        if (!best.kind || d < best.d) take = true;
-        else if (d == best.d)
-            take = (best.object == bvh.object) ? (S.tris[tri].rank > S.tris[best.index].rank) : (bvh.object < best.object);
-        else take = false;
-        if (take) {
+        // closest_intersection / min_by (the render kernel's takes_hit): branch-free on the kept rank
+        const uint32_t rk = (uint32_t)S.tris[tri].rank;
+        const bool closer = !best.kind | (d < best.d);
+        const bool tie = (d == best.d) & ((best.object == bvh.object) ? (rk > best.rank) : (bvh.object < best.object));
+        if (closer | tie) {
             best.d = d;
             best.kind = kTri;
             best.index = tri;
+            best.rank = rk;
             best.object = bvh.object;
             best.bary[0] = b[0];
             best.bary[1] = b[1];
@@ -737,6 +749,7 @@ __device__ __forceinline__ Best closest_hit(const DeviceScene& S, const RayPre& 
     best.kind = kNone;
     best.d = 0.0;
     best.index = -1;
+    best.rank = 0;
     best.object = 0x7fffffff;
     if (COUNT) cnt.rays++;
     // primitive lists, in object then position order: a later equal distance never wins (min_by)

@@ -215,8 +215,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     Best best;
     int node = -1, sp = 0, bvh_i = 0, cur_object = 0;
     int np = 0;  // this lane's queued leaf triangles not yet tested
-    // f32 forms of the cull thresholds: cull_far >= bound + margin (rounded up), cull_behind <=
-    // -behind_margin (rounded down; -inf when behind-culling is off) -- never tighter than f64
+    // f32 forms of the cull thresholds, widened by the ray's slab margin E (vr_device.h Ray32):
+    // cull_far >= bound + margin + E (rounded up), cull_behind <= -behind_margin - E (rounded down;
+    // -inf when behind-culling is off), compared with the slab values lo / hi as computed
     float cull_far = INFINITY, cull_behind = -INFINITY;
     int depth = -1, bounces = 0, flags = 0;
     double lambda = 0.0, T = 1.0, Acc = 0.0, T0 = 1.0, Acc0 = 0.0, b0 = 0.0, wo_y = 0.0;
@@ -230,10 +231,18 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     };
     auto set_cull_far = [&]() {
         const double bound = best.kind ? best.d : INFINITY;
-        const double t = bound + S.margin * (1.0 + fabs(bound));
-        float f = (float)t;
-        if ((double)f < t) f = nextafterf(f, INFINITY);
-        cull_far = f;
+        cull_far = round_away_f32(bound + S.margin * (1.0 + fabs(bound)) + margin_of(pre32));
+    };
+    // closest_intersection's rule for a triangle hit of the current BVH at distance d, reference rank
+    // rk: the smaller distance; at equal distances the later in-order leaf (higher rank) within the
+    // BVH, the earlier object across objects (sampler.rs min_by).  Branch-free selects on the rank
+    // kept in `best` (round 4: the nested branch form with a global load of the best triangle's rank
+    // was miscompiled in some builds -- a tie's new triangle index lost to the old one -- and the
+    // load was a dependent global access inside a divergent branch anyway)
+    auto takes_hit = [&](double d, uint32_t rk) {
+        const bool closer = !best.kind | (d < best.d);
+        const bool tie = (d == best.d) & ((best.object == cur_object) ? (rk > best.rank) : (cur_object < best.object));
+        return closer | tie;
     };
     // a queued leaf: its triangle index, bit 31 set when the leaf's f32 box test was too close to
     // call -- then the exact f64 line test on the triangle's own box (BoundingBox::from_points of
@@ -258,15 +267,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         double b[3];
         const double d = triangle_distance(tv, pre, b);
         if (d < 0.0) return;
-        bool take;
-        if (!best.kind || d < best.d) take = true;
-        else if (d == best.d)
-            take = (best.object == cur_object) ? (tv.rank > S.tris[best.index].rank) : (cur_object < best.object);
-        else take = false;
-        if (take) {
+        const uint32_t rk = (uint32_t)tv.rank;
+        if (takes_hit(d, rk)) {
             best.d = d;
             best.kind = kTri;
             best.index = tri;
+            best.rank = rk;
             best.object = cur_object;
             set_cull_far();
         }
@@ -349,15 +355,11 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const double dd = __longlong_as_double((long long)db);
                 const unsigned long long key = lr_key[tid];
                 const uint32_t rk = (uint32_t)(key >> 32);
-                bool take;
-                if (!best.kind || dd < best.d) take = true;
-                else if (dd == best.d)
-                    take = (best.object == cur_object) ? ((int64_t)rk > S.tris[best.index].rank) : (cur_object < best.object);
-                else take = false;
-                if (take) {
+                if (takes_hit(dd, rk)) {
                     best.d = dd;
                     best.kind = kTri;
                     best.index = (int)(uint32_t)key;
+                    best.rank = rk;
                     best.object = cur_object;
                     set_cull_far();
                 }
@@ -403,6 +405,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         best.kind = kNone;
         best.d = 0.0;
         best.index = -1;
+        best.rank = 0;
         best.object = 0x7fffffff;
         for (int i = 0; i < S.prim_count; ++i) {
             const Prim& pr = S.prims[i];
@@ -430,9 +433,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         }
         set_cull_far();
         if (pre.behind_ok()) {
-            float f = (float)(-S.behind_margin);
-            if ((double)f > -S.behind_margin) f = nextafterf(f, -INFINITY);
-            cull_behind = f;
+            cull_behind = round_away_f32(-S.behind_margin - margin_of(pre32));
         } else {
             cull_behind = -INFINITY;
         }
@@ -441,8 +442,18 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         state = start_bvhs() ? kTraversing : kTraversed;
     };
     // the sample's final photon goes to the staging buffer; accumulate_kernel turns it into XYZ
-    // (ColourXyz::from_photon of photon.scale_intensity(360)) and the Kahan sums
+    // (ColourXyz::from_photon of photon.scale_intensity(360)) and the Kahan sums.  finish() only
+    // notes the photon; phase A stores it at one place after shading (store_photon), so a wave whose
+    // lanes end their samples in different ways (camera miss, sky, recursion limit, early stop)
+    // runs the staging address arithmetic once, not once per way
+    bool fin = false;
+    double fin_wl = 0.0, fin_I = 0.0;
     auto finish = [&](double wl, double I) {
+        fin = true;
+        fin_wl = wl;
+        fin_I = I;
+    };
+    auto store_photon = [&](double wl, double I) {
         VR_SEC(6);
         VR_MARK("finish");
         double* out = A.staging + ((uint64_t)s_idx * npix + (uint64_t)py * A.tile_width + px) * 2;
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             ry.nx = __shfl(pre32.nx, owner);
             ry.ny = __shfl(pre32.ny, owner);
             ry.nz = __shfl(pre32.nz, owner);
-            ry.ek = __shfl(pre32.ek, owner);
+            ry.e2 = __shfl(pre32.e2, owner);
             const float cf = __shfl(cull_far, owner);
             const float cb = __shfl(cull_behind, owner);
             if (my >= 0) {
@@ -811,6 +822,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
                 bool go = false;
+                fin = false;
+#ifdef VR_DEBUG_PIX  // debug builds: one sample's traced rays and closest hits, for tools/debug_path.py
+                if ((A.start_row + py) * A.width + (A.start_column + px) == (uint64_t)VR_DEBUG_PIX &&
+                    A.first_sample + s_idx == (uint64_t)VR_DEBUG_SMP)
+                    printf("vrdbg %d %d %d %llx %llx %llx %llx %llx %llx %llx %d\n", depth, (int)best.kind, best.index,
+                           (unsigned long long)__double_as_longlong(best.d),
+                           (unsigned long long)__double_as_longlong(pre.o.x), (unsigned long long)__double_as_longlong(pre.o.y),
+                           (unsigned long long)__double_as_longlong(pre.o.z), (unsigned long long)__double_as_longlong(pre.d.x),
+                           (unsigned long long)__double_as_longlong(pre.d.y), (unsigned long long)__double_as_longlong(pre.d.z),
+                           best.kind == kTri ? (int)best.rank : -1);
+#endif
                 if (WHITTED && depth >= 0) {
                     if (!best.kind) {
                         finish(lambda, Acc);  // the continuation missed: photon.scale_intensity(0)
@@ -845,6 +867,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     }
                 }
                 if (go) shade();
+                if (fin) store_photon(fin_wl, fin_I);
             }
             VR_STAMP(0);
             VR_MARK("refill_check");
