@@ -452,13 +452,14 @@ __device__ __forceinline__ TriVerts load_tri(const TriVerts* p) {
 // v - o bitwise), permuted so the ray's largest signed component is last, sheared (z unscaled).
 __device__ __forceinline__ double triangle_distance(const TriVerts& t, const RayPre& p, double bary[3]) {
     const int k0 = p.k0(), k1 = p.k1(), k2 = p.k2();
-    const double ox = sel(p.o, k0), oy = sel(p.o, k1), oz = sel(p.o, k2);
     double tx[3], ty[3], az[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const V3 v = mk(t.v[3 * i], t.v[3 * i + 1], t.v[3 * i + 2]);
-        const double ax = sel(v, k0) + (-ox), ay = sel(v, k1) + (-oy);
-        az[i] = sel(v, k2) + (-oz);
+        // translated in the scene's axes, then permuted: sel(v + (-o), k) is sel(v, k) + (-sel(o, k))
+        // bit for bit, and the origin needs no selects of its own (12 v_cndmask per test)
+        const V3 a = mk(t.v[3 * i] + (-p.o.x), t.v[3 * i + 1] + (-p.o.y), t.v[3 * i + 2] + (-p.o.z));
+        const double ax = sel(a, k0), ay = sel(a, k1);
+        az[i] = sel(a, k2);
         tx[i] = ax + p.sx * az[i];
         ty[i] = ay + p.sy * az[i];
     }
@@ -480,8 +481,11 @@ __device__ __forceinline__ double triangle_distance(const TriVerts& t, const Ray
     tz = tz + az[1] * b1;
     tz = tz + az[2] * b2;
     if (sgn(tz) != sgn(p.pdz)) return -1.0;
-    V3 loc = mk(0.0, 0.0, 0.0);  // fold(Vec3::zeros()) (triangle.rs:66-71)
-    loc = add(loc, scl(mk(t.v[0], t.v[1], t.v[2]), b0));
+    // fold(Vec3::zeros()) (triangle.rs:66-71) without its first `0 +`: 0 + x differs from x only when
+    // x is -0 (+0), so the sums below differ from the reference's at most in the sign of a zero,
+    // which o - loc and the squares of the norm erase (o - (+-0) == o for o != 0; (+-0)^2 == +0):
+    // the distance's bits are the reference's (the hit location itself is recomputed for shading)
+    V3 loc = scl(mk(t.v[0], t.v[1], t.v[2]), b0);
     loc = add(loc, scl(mk(t.v[3], t.v[4], t.v[5]), b1));
     loc = add(loc, scl(mk(t.v[6], t.v[7], t.v[8]), b2));
     const V3 dv = sub(p.o, loc);
@@ -569,13 +573,12 @@ struct HitInfo {
 // the same operations up to b0..b2, without tz, the location and the distance's sqrt
 __device__ __forceinline__ void triangle_bary(const TriVerts& t, const RayPre& p, double bary[3]) {
     const int k0 = p.k0(), k1 = p.k1(), k2 = p.k2();
-    const double ox = sel(p.o, k0), oy = sel(p.o, k1), oz = sel(p.o, k2);
     double tx[3], ty[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const V3 v = mk(t.v[3 * i], t.v[3 * i + 1], t.v[3 * i + 2]);
-        const double ax = sel(v, k0) + (-ox), ay = sel(v, k1) + (-oy);
-        const double az = sel(v, k2) + (-oz);
+    for (int i = 0; i < 3; ++i) {  // translated, then permuted (as triangle_distance)
+        const V3 a = mk(t.v[3 * i] + (-p.o.x), t.v[3 * i + 1] + (-p.o.y), t.v[3 * i + 2] + (-p.o.z));
+        const double ax = sel(a, k0), ay = sel(a, k1);
+        const double az = sel(a, k2);
         tx[i] = ax + p.sx * az;
         ty[i] = ay + p.sy * az;
     }
