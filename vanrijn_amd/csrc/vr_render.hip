@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // leaf box bit for bit) decides whether the reference reaches the triangle at all
     auto test_tri = [&](int e) {
         const int tri = e & 0x7fffffff;
-        const TriVerts tv = load_tri(VR_TRIS + tri);
+        const TriVerts tv = load_tri((const TriVerts*)((const char*)VR_TRIS + (uint32_t)tri * (uint32_t)sizeof(TriVerts)));
         if (e < 0) {
             VR_SEC(2);
             VR_MARK("exact_box");
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // tests every flagged box, so its counters stay the reference's.
         TriVerts tv;
         if (mine) {
-            tv = load_tri(VR_TRIS + tri);
+            tv = load_tri((const TriVerts*)((const char*)VR_TRIS + (uint32_t)tri * (uint32_t)sizeof(TriVerts)));
             double b[3];
             d = triangle_distance(tv, op, b);  // needs the owner's shear constants, not its direction
             rank = (uint32_t)tv.rank;
@@ -1008,7 +1008,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
-                const Node4& nd = VR_NODES4[node];
+                // 32-bit byte offset from the scalar base (node < 2^25): the load's saddr form, no 64-bit
+                // address arithmetic per step
+                const Node4& nd = *(const Node4*)((const char*)VR_NODES4 + ((uint32_t)node << 7));
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
