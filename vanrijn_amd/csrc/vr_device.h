@@ -595,9 +595,10 @@ __device__ __forceinline__ void triangle_bary(const TriVerts& t, const RayPre& p
     bary[2] = ea2 * inv;
 }
 
-// full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96)
-// `dist`: the hit's distance from triangle_distance, sqrt((o - loc).(o - loc)) over the same loc
-// bits (triangle_bary repeats its operations), so the retro direction's norm is not recomputed
+// full Triangle::intersect for the winning triangle (shading data: triangle.rs:66-96).  `dist` (the
+// hit's distance, sqrt((o - loc).(o - loc)) over the same loc bits) is not needed: the retro direction
+// is normalised like the reference (dividing by `dist` instead gives the same bits but measured no
+// faster, round 2's VR_RETRO_DIST)
 __device__ void triangle_info(const TriVerts& t, const TriNormals& nn, const RayPre& p, double dist, HitInfo& h) {
     double b[3];
     triangle_bary(t, p, b);
