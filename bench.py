@@ -2,7 +2,13 @@
 """Benchmark: Msamples/s of the MI355X path-tracing core on BASELINE.json's headline config.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c5]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+--gpus N > 1 runs N ranks, one process per GPU: under `python -m torch.distributed.run
+--nproc-per-node N ... bench.py --gpus N ...` (the driver's launch) the ranks come from the
+environment; started directly, bench.py starts that launcher itself as ONE child process tree before
+anything touches the GPU (launch_ranks: never a re-exec), waits for it and forwards rank 0's JSON line.
+A WORLD_SIZE other than --gpus, or fewer GPUs on the node than --gpus, is an error (exit status 2),
+never a silent smaller run; `n_gpus` is the process group's dist.get_world_size().
 
 Workload (default --config c3 = BASELINE.json configs[2] / metric): the main.rs scene
 (src/main.rs:120-189: plane, three spheres, Lambertian bunny; camera (-2, 1, -5)) at 1024x1024,
@@ -175,7 +181,12 @@ PMC_PASSES = [
     ("mix2", ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
               "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "SQ_WAVES"]),
     ("tcc", ["TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE"]),
+    # hardware VALU activity and lane use: the cycles waves spend issuing VALU, and
+    # the lane-cycles of work they did; with this pass's own clock (GRBM_GUI_ACTIVE, 8 XCDs)
+    ("lanes", ["SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]),
 ]
+# counters a pass repeats from another, kept under "<name>@<pass>"
+PMC_PASS_LOCAL = {"lanes": ("SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")}
 
 
 def _is_timed_render(name):
@@ -230,6 +241,9 @@ def live_pmc(child_args, timeout_s=150):
             if rc != 0:
                 return {"error": f"PMC pass {name} exited {rc}"}
             c, ns = _fold_pass(d)
+            for k in PMC_PASS_LOCAL.get(name, ()):
+                if k in c:
+                    c[f"{k}@{name}"] = c.pop(k)
             per_launch.update(c)
             if ns:
                 kernel_ns[name] = ns
@@ -297,6 +311,13 @@ def roofline(counts, pixels, kernel_s, key, passes=1, pmc=None):
         if pmc.get("SQ_WAVE_CYCLES") else None,
         "l2_hit_rate": round(pmc["TCC_HIT_sum"] / (pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"]), 4)
         if "TCC_HIT_sum" in pmc else None,
+        # measured, not priced: 4 SQ_ACTIVE_INST_VALU per SIMD-cycle of the profiled
+        # launch (GRBM_GUI_ACTIVE / 8 XCDs) -- the VALU-busy fraction of all 1024 SIMDs -- and the lane
+        # efficiency of what was issued, SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)
+        "valu_active_frac": round(4 * pmc["SQ_ACTIVE_INST_VALU"] / (SIMDS * pmc["GRBM_GUI_ACTIVE@lanes"] / 8), 4)
+        if pmc.get("GRBM_GUI_ACTIVE@lanes") else None,
+        "valu_lane_efficiency": round(pmc["SQ_THREAD_CYCLES_VALU"] / (64 * pmc["SQ_ACTIVE_INST_VALU"]), 4)
+        if pmc.get("SQ_ACTIVE_INST_VALU") else None,
         "profiled_clock_ghz": round(clk, 3),
         "profiled_kernel_ms": round(rec["kernel_ns"] / 1e6, 3),
         "pmc": rec.get("source"),
@@ -412,6 +433,58 @@ def drop_in_leg(dscene, width, height, frames, threads, device):
                        "buffers: 88 B/pixel back over PCIe), vr_merge_tile on the main thread"}
 
 
+# ---------------------------------------------------------------------------- rank launcher
+def launch_ranks(argv, n, stub=False):
+    """`--gpus n` (n > 1) started without torch.distributed.run's environment: start
+    `python -m torch.distributed.run --nproc-per-node n ... bench.py <argv>` as one child process tree
+    (one fresh process per GPU: this process has not touched the GPU -- torch.cuda.device_count()
+    does not initialise it on this image -- and it is never replaced by exec), wait, and forward the
+    JSON line rank 0 prints.  Returns the exit status.  `stub`: the CPU test of this launcher (gloo
+    ranks, tests/test_bench_launcher.py), no GPU count check."""
+    import socket
+    import subprocess
+    if not stub:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} GPUs on this node, found {have}; refusing to report a "
+                  f"{have}-GPU run as {n}", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as sk:  # a free rendezvous port on the loopback address
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    print("bench.py: starting " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    lines = []
+    for line in p.stdout:  # rank 0's JSON line; anything else goes to stderr
+        if line.lstrip().startswith("{"):
+            lines.append(line.strip())
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc == 0 and len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr, flush=True)
+        return 1
+    for line in lines:
+        print(line, flush=True)
+    return rc
+
+
+def stub_rank_body():
+    """A rank body without the GPU (launcher test): a gloo group, each rank's view of its launch
+    environment gathered on rank 0, which prints one JSON line."""
+    dist.init_process_group("gloo")
+    mine = {k: int(os.environ[k]) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    mine["pid"] = os.getpid()
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, mine)
+    if dist.get_rank() == 0:
+        print(json.dumps({"stub": True, "n_gpus": dist.get_world_size(), "ranks": got}), flush=True)
+    dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -439,7 +512,19 @@ def main():
     ap.add_argument("--host-build", action="store_true",
                     help="render the host-built traversal tree instead of the device-built one (same images)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
+    ap.add_argument("--stub-ranks", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU, gloo)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "RANK" not in os.environ and args.gpus > 1:  # start the ranks (nothing has touched the GPU yet)
+        return launch_ranks(sys.argv[1:], args.gpus, stub=args.stub_ranks)
+    if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", 1)) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {os.environ.get('WORLD_SIZE')}: refusing to run a "
+              f"different number of ranks than asked for", file=sys.stderr, flush=True)
+        return 2
+    if args.stub_ranks:
+        stub_rank_body()
+        return 0
     if args.pmc_child:
         args.steps, args.warmup, args.no_drop_in, args.no_cpu_baseline, args.no_pmc = 1, 0, True, True, True
 
@@ -450,14 +535,14 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     # launched by torch.distributed.run (RANK set): the RCCL group is created even at world size 1,
     # so a one-GPU box rehearses the multi-GPU step (init, barriers, reduce, max-over-ranks timing)
     distributed = world > 1 or "RANK" in os.environ
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()  # what the line reports as n_gpus
+        assert world == args.gpus, (world, args.gpus)
 
     W, H = cfg["width"], cfg["height"]
     spp = D.shard_spp(cfg["spp"], world, cfg["split"])  # this rank's samples per pixel per frame
@@ -594,4 +679,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

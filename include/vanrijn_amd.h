@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 7
+#define VR_ABI_VERSION 8
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -171,6 +171,11 @@ typedef struct vr_scene vr_scene;
  * child expanded first) instead of by the SAH-optimal dynamic programme.
  * Renders are identical either way; for inspection and the collapse's own tests (ABI 7). */
 #define VR_SCENE_GREEDY_COLLAPSE 16u
+/* Render with the 64-bit-offset kernels whatever the scene's size (ABI 8).  They are chosen
+ * automatically for scenes past the 32-bit load offsets of the default kernels -- 4 GB of triangle
+ * records (53.7 M triangles) or 2^25 nodes of the 4-wide tree (vr_scene_needs_wide_offsets); this
+ * flag exercises them on small scenes (tests).  Renders are identical either way. */
+#define VR_SCENE_WIDE_OFFSETS 32u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split
@@ -268,7 +273,11 @@ typedef struct vr_launch_stats {
     uint64_t exact_box_tests;  /* f32 box tests too close to call, re-run exactly in f64 */
     float reduce_ms;           /* HIP-event time of the ordered per-pixel Kahan reduce(s) (timed) */
     uint32_t passes;           /* render + reduce launches (the staging buffer bounds a launch) */
+    uint32_t variant;          /* VR_VARIANT_* bits of the render kernel that ran (ABI 8) */
+    uint32_t reserved;
 } vr_launch_stats;
+#define VR_VARIANT_COOP 1u         /* the cooperative-tail instantiation (small launches, mirror scenes) */
+#define VR_VARIANT_WIDE_OFFSETS 2u /* the 64-bit-offset kernels (VR_SCENE_WIDE_OFFSETS) */
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */
 #define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
@@ -280,6 +289,13 @@ typedef struct vr_launch_stats {
 /* skip the camera-frustum culling of 8x8 pixel blocks (every sample traced): the records are the
  * same bit for bit (tests/test_gpu_cull.py); for tests and A/B measurements (ABI 7) */
 #define VR_LAUNCH_NO_CULL 8u
+/* no BVH distance culling: every box the ray's line crosses is walked (the reference's exhaustive
+ * traversal, bounding_volume_hierarchy.rs:94-120), with the same records bit for bit -- the check
+ * that the tie rule does not lean on the culling order (tests/test_gpu_nocull_ties.py; ABI 8) */
+#define VR_LAUNCH_NO_DIST_CULL 16u
+/* no cooperative tail (small launches of scenes with a reflective material otherwise spread a
+ * wave's last one or two paths over its lanes): the same records bit for bit (ABI 8) */
+#define VR_LAUNCH_NO_COOP 32u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
@@ -375,6 +391,14 @@ int vr_scene_set_staging_limit(vr_scene* scene, uint64_t bytes);
  * which finite geometry cannot reach; -1 turns it off.  Not thread-safe against concurrent render
  * calls on the same scene: set it before rendering (tests/test_gpu_concurrency.py).  ABI 5. */
 int vr_debug_set_fault_object(vr_scene* scene, int32_t object);
+
+/* Test hook: launch flags (VR_LAUNCH_NO_CULL / _NO_DIST_CULL / _NO_COOP only) applied to every render
+ * call of the scene, including the host-buffer and per-sample record entry points that take no launch
+ * flags of their own; 0 turns them off.  Set before rendering, like the fault object (ABI 8). */
+int vr_debug_set_launch_flags(vr_scene* scene, uint32_t flags);
+/* 1 when a scene with this many triangles and 4-wide nodes renders with the 64-bit-offset kernels
+ * (VR_SCENE_WIDE_OFFSETS), else 0.  Host only, no device (ABI 8). */
+int vr_scene_needs_wide_offsets(uint64_t triangle_count, uint64_t wide_node_count);
 
 int vr_device_count(void);
 const char* vr_last_error(void);

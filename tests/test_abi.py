@@ -37,12 +37,42 @@ def test_struct_sizes_match_header():
     assert C.sizeof(N.SampleRecord) == 48
     assert C.sizeof(N.HitRecord) == 144
     assert C.sizeof(N.LaunchTimes) == 32
+    assert C.sizeof(N.LaunchStats) == 96
 
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 7
+    assert lib.vr_abi_version() == 8
     assert isinstance(lib.vr_last_error(), bytes)
+
+
+def test_wide_offset_limits():
+    """The default kernels address triangles (80-B TriVerts) and 4-wide nodes (128 B) with 32-bit
+    byte offsets; past 4 GB of triangles or 2^25 wide nodes a scene takes the 64-bit-offset kernels
+    (vr_render.hip render_kernel<.., BIG>; ADVICE r04: before, such a mesh silently read the wrong
+    records).  Host only: the choice, at and either side of both limits."""
+    f = N.lib().vr_scene_needs_wide_offsets
+    tri_limit = (1 << 32) // 80 + 1  # the first count whose last record's offset reaches 2^32
+    assert f(tri_limit - 1, 0) == 0 and f(tri_limit, 0) == 1
+    assert f(53_687_091, 0) == 0 and f(53_687_092, 0) == 1
+    assert f(1_051_392, 413_444) == 0  # C5's mesh and tree
+    assert f(1000, (1 << 25) - 1) == 0 and f(1000, 1 << 25) == 1
+    assert f((1 << 31) - 1, 1 << 30) == 1
+
+
+def test_debug_launch_flags_validated():
+    """vr_debug_set_launch_flags takes only the flags that leave records bit-identical."""
+    from vanrijn_amd import scenes
+    ds = scenes.bench_scene(scenes.displaced_mesh(6, [], 1, 0, 0.0, (1, 1, 1), (0, 0, 0))).device_scene(
+        0, host_only=True)
+    ds.set_launch_flags(no_cull=True, no_dist_cull=True, no_coop=True)
+    ds.set_launch_flags()
+    try:
+        N.check(N.lib().vr_debug_set_launch_flags(ds.handle, N.LAUNCH_TIMED))
+    except N.VrError as e:
+        assert e.code == -1
+    else:
+        raise AssertionError("a timing flag is not a scene-wide debug flag")
 
 
 def test_host_only_scene_and_errors():

@@ -155,6 +155,13 @@ def _keep_worker(rank, world, port, out_path):
         # the collective works in place: a non-destination rank's sums half is the collective's
         # (gloo uses it as scratch), its compensations are untouched
         assert torch.equal(rec[20:], mine[20:])
+    # keep_local: the collective runs on a copy on the other ranks, whose records stay their own
+    rec2 = torch.arange(5 * 8, dtype=torch.float64) + 100 * rank
+    D.reduce_records(rec2, keep_local=True)
+    if rank == 0:
+        assert torch.equal(rec2, want)
+    else:
+        assert torch.equal(rec2, mine)
     np.save(f"{out_path}.{rank}.npy", rec.numpy())
     dist.barrier()
     dist.destroy_process_group()
@@ -164,3 +171,26 @@ def test_reduce_destination_and_other_ranks(tmp_path):
     out = str(tmp_path / "keep")
     mp.spawn(_keep_worker, args=(3, _free_port(), out), nprocs=3, join=True)
     assert all(os.path.exists(f"{out}.{r}.npy") for r in range(3))
+
+
+def test_accumulation_buffer_from_state_shapes():
+    """from_state takes the flat ABI-7 records with width / height, or a [h][w][8] array of them; a
+    size that does not fit raises instead of misreading."""
+    from vanrijn_amd.render import AccumulationBuffer
+    rng = np.random.default_rng(4)
+    f = {"colour_sum": rng.uniform(1, 2, size=(H, W, 3)), "colour_bias": rng.normal(size=(H, W, 3)) * 1e-17,
+         "weight": rng.integers(1, 9, size=(H, W)).astype(float), "weight_bias": np.zeros((H, W))}
+    flat = R.from_fields(**f)
+    a = AccumulationBuffer.from_state(flat, W, H)
+    b = AccumulationBuffer.from_state(flat.reshape(H, W, 8))
+    c = AccumulationBuffer.from_state(torch.from_numpy(flat), W, H)
+    for x in (b, c):
+        assert np.array_equal(a.colour_buffer, x.colour_buffer) and np.array_equal(a.weight_buffer, x.weight_buffer)
+    assert np.array_equal(a.colour_sum_buffer, f["colour_sum"])
+    for bad in ((flat, W + 1, H), (flat.reshape(H, W * 8), None, None), (flat[: 8 * H * W - 8], W, H)):
+        try:
+            AccumulationBuffer.from_state(*bad)
+        except ValueError:
+            pass
+        else:
+            raise AssertionError("a record array of the wrong size must raise")

@@ -19,10 +19,19 @@ which = sys.argv[2] if len(sys.argv) > 2 else "main"
 torch.cuda.set_device(0)
 ds = (scenes.main_scene() if which == "main" else scenes.bench_scene()).device_scene(0)
 state = torch.zeros(1024 * 1024 * 8, dtype=torch.float64, device="cuda")
-path = os.path.join("gpurun_out", "counters.bin")
+# an absolute path under the repository (the box runs from a scratch copy; a relative path depended
+# on the working directory and on gpurun_out/ existing), removed first so a stale file never answers
+out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+os.makedirs(out_dir, exist_ok=True)
+path = os.path.join(out_dir, "counters.bin")
+if os.path.exists(path):
+    os.remove(path)
 os.environ["VR_COUNTERS_PATH"] = path
 st = render_tile_device(ds, Tile(0, 1024, 0, 1024), 1024, 1024, spp, 1, 0, state.data_ptr(),
                         torch.cuda.current_stream().cuda_stream, counters=True)
+if not os.path.exists(path):
+    sys.exit("tools/cycles.py: no counters written -- the library is not a tuning build "
+             "(VR_LIBRARY=<a -DVR_TUNING_VARIANTS build>, see the docstring)")
 c = np.fromfile(path, dtype=np.uint64)
 cyc = c[9:15].astype(np.float64)
 out = {"scene": which, "spp": spp, "kernel_ms": st["kernel_ms"],

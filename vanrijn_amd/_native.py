@@ -24,7 +24,10 @@ SCENE_DEVICE_BVH = 2
 SCENE_REFERENCE_BVH = 4
 SCENE_DEVICE_SAH = 8
 SCENE_GREEDY_COLLAPSE = 16
+SCENE_WIDE_OFFSETS = 32
 LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES, LAUNCH_NO_CULL = 1, 2, 4, 8
+LAUNCH_NO_DIST_CULL, LAUNCH_NO_COOP = 16, 32
+VARIANT_COOP, VARIANT_WIDE_OFFSETS = 1, 2
 SCENE_INFO_NAN_FREE = 1
 
 
@@ -108,10 +111,10 @@ class LaunchStats(C.Structure):
                 ("node_visits", C.c_uint64), ("triangle_tests", C.c_uint64), ("rays", C.c_uint64),
                 ("shaded_triangle_hits", C.c_uint64), ("samples", C.c_uint64), ("traversal_slots", C.c_uint64),
                 ("path_loop_slots", C.c_uint64), ("exact_box_tests", C.c_uint64), ("reduce_ms", C.c_float),
-                ("passes", C.c_uint32)]
+                ("passes", C.c_uint32), ("variant", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
 
 
 class LaunchTimes(C.Structure):
@@ -161,6 +164,8 @@ SIGNATURES = {
     "vr_write_png": (C.c_int, [C.c_char_p, _p, _u32, _u32]),
     "vr_scene_set_staging_limit": (C.c_int, [_p, _u64]),
     "vr_debug_set_fault_object": (C.c_int, [_p, _i32]),
+    "vr_debug_set_launch_flags": (C.c_int, [_p, _u32]),
+    "vr_scene_needs_wide_offsets": (C.c_int, [_u64, _u64]),
     "vr_device_count": (C.c_int, []),
     "vr_last_error": (C.c_char_p, []),
     "vr_abi_version": (C.c_uint32, []),

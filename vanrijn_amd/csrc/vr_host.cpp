@@ -538,6 +538,7 @@ struct vr_scene {
     bool device_bvh = false;
     bool device_sah = false;  // VR_SCENE_DEVICE_SAH: the SAH traversal tree too (vr_build.hip)
     bool greedy_collapse = false;  // VR_SCENE_GREEDY_COLLAPSE: the 4-wide tree by largest child area
+    bool force_big = false;        // VR_SCENE_WIDE_OFFSETS: the 64-bit-offset kernels for any size
     uint64_t staging_limit = 0;    // vr_scene_set_staging_limit: bytes of staging per call (0: half the free HBM)
     uint64_t node_count = 0, tri_count = 0;
     struct PendingMesh {
@@ -584,7 +585,19 @@ struct vr_scene {
     // test hook (vr_debug_set_fault_object): hits on this object take the singular-basis path,
     // which finite geometry cannot reach (DESIGN.md "Errors")
     int32_t fault_object = -1;
+    // test hook (vr_debug_set_launch_flags): launch flags OR'ed into every render of the scene
+    uint32_t debug_launch_flags = 0;
 };
+
+// The render kernel addresses the triangle and 4-wide node arrays with 32-bit byte offsets from
+// their scalar bases (tri * 80, node << 7); a scene past either limit -- 53.7 M triangles (4 GB of
+// TriVerts), 2^25 wide nodes -- runs the kernels with 64-bit offsets (render_kernel<.., BIG>)
+static bool needs_big_offsets(uint64_t tri_count, uint64_t wide_count) {
+    return tri_count * sizeof(vr::TriVerts) >= (1ull << 32) || wide_count >= (1ull << 25);
+}
+static bool needs_big_offsets(const vr_scene* s) {
+    return s->force_big || needs_big_offsets(s->tri_count, s->wide_count);
+}
 
 // One render call's device resources.  `done` is recorded on the launch stream after the last
 // kernel that reads `staging` / `queue`; a later user of the context waits on it first.
@@ -1307,6 +1320,7 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     s->device = device;
     s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
     s->greedy_collapse = (flags & VR_SCENE_GREEDY_COLLAPSE) != 0;
+    s->force_big = (flags & VR_SCENE_WIDE_OFFSETS) != 0;
     s->camera[0] = desc->camera_location.x;
     s->camera[1] = desc->camera_location.y;
     s->camera[2] = desc->camera_location.z;
@@ -1627,6 +1641,18 @@ int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
     return VR_OK;
 }
 
+int vr_debug_set_launch_flags(vr_scene* s, uint32_t flags) {
+    if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
+    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP;
+    if (flags & ~allowed) return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP apply to every call");
+    s->debug_launch_flags = flags;
+    return VR_OK;
+}
+
+int vr_scene_needs_wide_offsets(uint64_t triangle_count, uint64_t wide_node_count) {
+    return needs_big_offsets(triangle_count, wide_node_count) ? 1 : 0;
+}
+
 int vr_scene_bvh_nodes(const vr_scene* s, void* out) {
     if (!s || !out) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
     const size_t bytes = s->node_count * sizeof(vr::Node);
@@ -1684,7 +1710,10 @@ int grid_per_cu() {
 
 int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* state, hipStream_t st, int32_t* err,
                    bool counting, bool recording, void* records, unsigned long long* counters,
-                   unsigned long long* wg_times, PassEvents* timing = nullptr, bool no_cull = false) {
+                   unsigned long long* wg_times, PassEvents* timing = nullptr, uint32_t launch_flags = 0,
+                   uint32_t* variant = nullptr) {
+    launch_flags |= s->debug_launch_flags;
+    const bool no_cull = (launch_flags & VR_LAUNCH_NO_CULL) != 0;
     const uint64_t tw = p->tile.end_column - p->tile.start_column, th = p->tile.end_row - p->tile.start_row;
     const uint64_t npix = tw * th;
     if (npix == 0 || p->spp == 0) return VR_OK;
@@ -1742,6 +1771,13 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         q.accumulate = (done > 0 || p->accumulate) ? 1u : 0u;
         vr::RenderArgs a = make_args(s, &q, state);
         a.staging = (double*)c->staging;
+        if (launch_flags & VR_LAUNCH_NO_DIST_CULL) {
+            // every box the line crosses is walked (culled() / cull_far / cull_behind never prune):
+            // the records stay the same bit for bit (tests/test_gpu_nocull_ties.py)
+            a.scene.margin = INFINITY;
+            a.scene.behind_margin = INFINITY;
+        }
+        if (launch_flags & VR_LAUNCH_NO_COOP) a.coop = 0;
 #ifdef VR_STAGE_GUARD
         a.stage_tag = (uint32_t*)c->tags;
         if (++c->gen == 0) c->gen = 1;
@@ -1765,8 +1801,18 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         }
         // LDS stack entries: the 4-wide walk's, and the binary walk's for Whitted shadow rays
         const int stack = s->dev.integrator == 1 ? std::max(stack_depth(s), wide_stack_depth(s)) : wide_stack_depth(s);
-        int lr = vr::launch_render(a, stack, counting, recording, s->dark0, s->mats ? s->mats : 3,
-                                   std::max(1, s->cu_count) * grid_per_cu(), st, mid);
+        vr::LaunchChoice lc;
+        lc.stack_depth = stack;
+        lc.counting = counting;
+        lc.recording = recording;
+        lc.dark0 = s->dark0;
+        lc.mats = s->mats ? s->mats : 3;
+        lc.big = needs_big_offsets(s);
+        // the cooperative tail's instantiations exist for DARK0 scenes with a reflective material
+        lc.coop = a.coop != 0 && !recording && !counting && !lc.big && s->dev.integrator != 1 && s->dark0 &&
+                  (lc.mats & 2);
+        if (variant) *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u);
+        int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * grid_per_cu(), st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {
             hipEvent_t end = timing->add();
@@ -1826,15 +1872,22 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         if (wg_path) VR_HIP(hipMalloc(&wg.ptr, blocks * 2 * sizeof(unsigned long long)));
     }
     PassEvents pe;
+    uint32_t variant = 0;
     {
         CtxLease L(ms);
         rc = ctx_acquire(ms, &L.c, &st);
         if (rc) return rc;
         rc = enqueue_passes(ms, L.c, p, state, st, slot, counting, false, nullptr, counters,
-                            (unsigned long long*)wg.ptr, timed ? &pe : nullptr, (launch_flags & VR_LAUNCH_NO_CULL) != 0);
+                            (unsigned long long*)wg.ptr, timed ? &pe : nullptr, launch_flags, &variant);
         if (rc) return rc;
     }
-    if (!timed) return VR_OK;  // errors of this launch: vr_stream_check_error(scene, stream)
+    if (!timed) {  // errors of this launch: vr_stream_check_error(scene, stream)
+        if (stats) {
+            std::memset(stats, 0, sizeof *stats);
+            stats->variant = variant;
+        }
+        return VR_OK;
+    }
     if (defer) {
         std::lock_guard<std::mutex> g(ms->slot_mutex);
         vr_scene::Deferred& d = ms->deferred[stream];
@@ -1844,6 +1897,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         if (stats) {
             std::memset(stats, 0, sizeof *stats);
             stats->passes = d.passes.back();
+            stats->variant = variant;
         }
         return VR_OK;
     }
@@ -1861,6 +1915,7 @@ int vr_render_tile_device(const vr_scene* s, const vr_render_params* p, double* 
         stats->kernel_ms = render_ms;
         stats->reduce_ms = reduce_ms;
         stats->passes = (uint32_t)(pe.ev.size() / 3);
+        stats->variant = variant;
         stats->timed = 1;
     }
     if (counting) {

@@ -217,8 +217,19 @@ enum Counter : int {
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
-int launch_render(const RenderArgs& args, int stack_depth, bool counting, bool recording, bool dark0, int mats,
-                  int grid_limit, void* stream, void* mid_event = nullptr);
+// Which render_kernel instantiation a launch runs (vr_host.cpp enqueue_passes picks, vr_render.hip
+// launch_render maps it to the template).
+struct LaunchChoice {
+    int stack_depth;  // LDS stack entries the scene's traversal needs (class 24 / 32 / 48)
+    bool counting;    // the counting variant (VR_LAUNCH_COUNTERS)
+    bool recording;   // the per-sample record variant (vr_render_samples)
+    bool dark0;       // every material's colour at 0 nm is 0
+    int mats;         // material kinds present (bit 0 Lambertian, 1 reflective, 2 Phong / dielectric)
+    bool coop;        // the cooperative-tail instantiation (RenderArgs::coop set; never with the above)
+    bool big;         // 64-bit node / triangle load offsets (vr_host.cpp needs_big_offsets)
+};
+int launch_render(const RenderArgs& args, const LaunchChoice& choice, int grid_limit, void* stream,
+                  void* mid_event = nullptr);
 // vr_image.hip: records (from_state = 1, RenderArgs::state's layout) or XYZ colour (3 f64) -> sRGB8
 // the camera-frustum test of every 8x8 block of a launch's tile into mask (RenderArgs::block_mask)
 int launch_block_cull(const RenderArgs& args, uint8_t* mask, void* stream);

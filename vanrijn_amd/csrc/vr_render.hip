@@ -143,8 +143,11 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
 // COOP: the cooperative tail (coop_step below) -- instantiated for the small launches of scenes with
 // a reflective material, the only ones whose time is a few trapped paths (vr_host.cpp make_args).
+// BIG: 64-bit byte offsets for the node and triangle loads -- scenes whose triangle array reaches 4 GB
+// (53.7 M triangles) or whose 4-wide tree has 2^25 nodes (vr_host.cpp needs_big_offsets); every other
+// scene's kernels address both arrays with 32-bit offsets from the scalar base (the loads' saddr form)
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          bool COOP = false>
+          bool COOP = false, bool BIG = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -239,6 +242,15 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // kept in `best` (round 4: the nested branch form with a global load of the best triangle's rank
     // was miscompiled in some builds -- a tie's new triangle index lost to the old one -- and the
     // load was a dependent global access inside a divergent branch anyway)
+    // the triangle record of leaf link ~tri and the 4-wide node `n`
+    auto tri_at = [&](int tri) -> const TriVerts* {
+        if (BIG) return VR_TRIS + (uint32_t)tri;
+        return (const TriVerts*)((const char*)VR_TRIS + (uint32_t)tri * (uint32_t)sizeof(TriVerts));
+    };
+    auto node_at = [&](int n) -> const Node4& {
+        if (BIG) return VR_NODES4[(uint32_t)n];
+        return *(const Node4*)((const char*)VR_NODES4 + ((uint32_t)n << 7));
+    };
     auto takes_hit = [&](double d, uint32_t rk) {
         const bool closer = !best.kind | (d < best.d);
         const bool tie = (d == best.d) & ((best.object == cur_object) ? (rk > best.rank) : (cur_object < best.object));
@@ -250,7 +262,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // leaf box bit for bit) decides whether the reference reaches the triangle at all
     auto test_tri = [&](int e) {
         const int tri = e & 0x7fffffff;
-        const TriVerts tv = load_tri((const TriVerts*)((const char*)VR_TRIS + (uint32_t)tri * (uint32_t)sizeof(TriVerts)));
+        const TriVerts tv = load_tri(tri_at(tri));
         if (e < 0) {
             VR_SEC(2);
             VR_MARK("exact_box");
@@ -312,7 +324,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // tests every flagged box, so its counters stay the reference's.
         TriVerts tv;
         if (mine) {
-            tv = load_tri((const TriVerts*)((const char*)VR_TRIS + (uint32_t)tri * (uint32_t)sizeof(TriVerts)));
+            tv = load_tri(tri_at(tri));
             double b[3];
             d = triangle_distance(tv, op, b);  // needs the owner's shear constants, not its direction
             rank = (uint32_t)tv.rank;
@@ -738,7 +750,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             const float cf = __shfl(cull_far, owner);
             const float cb = __shfl(cull_behind, owner);
             if (my >= 0) {
-                const Node4& nd = VR_NODES4[my];
+                const Node4& nd = node_at(my);
                 if (COUNT) cnt.node_visits++;
                 uint32_t xm = 0;
 #pragma unroll
@@ -1008,9 +1020,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
                 VR_MARK("node_step");
-                // 32-bit byte offset from the scalar base (node < 2^25): the load's saddr form, no 64-bit
-                // address arithmetic per step
-                const Node4& nd = *(const Node4*)((const char*)VR_NODES4 + ((uint32_t)node << 7));
+                // 32-bit byte offset from the scalar base (node < 2^25 unless BIG): the load's saddr form,
+                // no 64-bit address arithmetic per step
+                const Node4& nd = node_at(node);
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
@@ -1456,76 +1468,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs A) {
 // ----------------------------------------------------------------------------------------------
 // Host-side launch wrappers
 // ----------------------------------------------------------------------------------------------
-template <int STACK>
-static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recording, bool dark0, int mats,
-                                  int grid_limit, hipStream_t s, hipEvent_t mid) {
-    // persistent waves: enough workgroups to fill the chip, each wave loops over work items
-    const uint64_t items = dev::render_items(a, ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64);
-    const uint64_t want = (items + 255) / 256;
-    dim3 grid((unsigned)(want < (uint64_t)grid_limit ? want : (uint64_t)grid_limit)), block(256);
-    // kinds present (bit 0 Lambertian, 1 reflective, 2 Phong or dielectric) -> specialisation:
-    // Lambertian-only (1), reflective-only (2) or the general kernel (3)
-    mats = (mats == 1 || mats == 2) ? mats : 3;
-    if (!dark0) mats = 3;  // the general kernel
-#ifdef VR_TUNING_VARIANTS  // experiment hooks of tuning builds only (tools/variants.py)
-    // 1..4 = force that many waves per SIMD (default 3); VR_FORCE_MATS: the material specialisation
-    const char* ve = getenv("VR_KERNEL_VARIANT");
-    const int variant = ve ? atoi(ve) : 0;
-    if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);
-#endif
-    if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
-        if (recording) hipLaunchKernelGGL((dev::render_kernel<STACK, false, true, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
-        else if (counting) hipLaunchKernelGGL((dev::render_kernel<STACK, true, false, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
-        else hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, true, 3, 3, true>), grid, block, 0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (mid) {
-            e = hipEventRecord(mid, s);
-            if (e != hipSuccess) return e;
-        }
-        const uint64_t npix = a.tile_width * a.tile_height;
-        hipLaunchKernelGGL(dev::accumulate_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a.state,
-                           (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width,
-                       a.stage_tag, a.stage_gen, a.error_flag);
-        return hipGetLastError();
-    }
-#define VR_LAUNCH(C, R, D, M, W)                                                                      \
-    hipLaunchKernelGGL((dev::render_kernel<STACK, C, R, D, M, W>), grid, block, 0, s, a, a.scene.prims, \
-                       a.scene.materials, a.scene.bvhs)
-    // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
-    // of scenes with a reflective material)
-#define VR_LAUNCH_COOP(D, M)                                                                                 \
-    hipLaunchKernelGGL((dev::render_kernel<STACK, false, false, D, M, 3, false, true>), grid, block, 0, s, a, \
-                       a.scene.prims, a.scene.materials, a.scene.bvhs)
-#ifdef VR_TUNING_VARIANTS  // occupancy experiments (python -m vanrijn_amd.build with VR_TUNING=1)
-#define VR_MODES(D, M)                                     \
-    if (recording) VR_LAUNCH(false, true, D, M, 3);        \
-    else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
-    else if (variant == 1) VR_LAUNCH(false, false, D, M, 1); \
-    else if (variant == 2) VR_LAUNCH(false, false, D, M, 2); \
-    else if (variant == 4) VR_LAUNCH(false, false, D, M, 4); \
-    else VR_LAUNCH(false, false, D, M, 3)
-#else
-#define VR_MODES(D, M)                                     \
-    if (recording) VR_LAUNCH(false, true, D, M, 3);        \
-    else if (counting) VR_LAUNCH(true, false, D, M, 3);    \
-    else VR_LAUNCH(false, false, D, M, 3)
-#endif
-    const bool coop = a.coop != 0 && !recording && !counting;
-    if (!dark0) {
-        VR_MODES(false, 3);
-    } else if (mats == 1) {
-        VR_MODES(true, 1);
-    } else if (mats == 2) {
-        if (coop) VR_LAUNCH_COOP(true, 2);
-        else VR_MODES(true, 2);
-    } else {
-        if (coop) VR_LAUNCH_COOP(true, 3);
-        else VR_MODES(true, 3);
-    }
-#undef VR_MODES
-#undef VR_LAUNCH_COOP
-#undef VR_LAUNCH
+static hipError_t launch_reduce(const RenderArgs& a, hipStream_t s, hipEvent_t mid) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (mid) {  // between the render kernel and the ordered reduce (timed launches)
@@ -1537,6 +1480,79 @@ static hipError_t launch_render_t(const RenderArgs& a, bool counting, bool recor
                        (const double*)a.staging, npix, a.spp, a.accumulate, a.block_mask, a.tile_width,
                        a.stage_tag, a.stage_gen, a.error_flag);
     return hipGetLastError();
+}
+
+template <int STACK>
+static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, int grid_limit, hipStream_t s,
+                                  hipEvent_t mid) {
+    // persistent waves: enough workgroups to fill the chip, each wave loops over work items
+    const uint64_t items = dev::render_items(a, ((a.tile_width + 7) / 8) * ((a.tile_height + 7) / 8) * 64);
+    const uint64_t want = (items + 255) / 256;
+    dim3 grid((unsigned)(want < (uint64_t)grid_limit ? want : (uint64_t)grid_limit)), block(256);
+    const bool recording = c.recording, counting = c.counting;
+#define VR_K(...) hipLaunchKernelGGL((dev::render_kernel<__VA_ARGS__>), grid, block, 0, s, a, a.scene.prims, \
+                                     a.scene.materials, a.scene.bvhs)
+    if (c.big) {
+        // 64-bit load offsets (scenes past 4 GB of triangles or 2^25 wide nodes): the general
+        // kernels only (DARK0 = false and every material kind are always correct, only slower), in
+        // the deepest stack class only (launch_render)
+        if constexpr (STACK != 48) return hipErrorInvalidValue;
+        else if (a.scene.integrator == 1) {
+            if (recording) VR_K(STACK, false, true, false, 3, 3, true, false, true);
+            else if (counting) VR_K(STACK, true, false, false, 3, 3, true, false, true);
+            else VR_K(STACK, false, false, false, 3, 3, true, false, true);
+        } else {
+            if (recording) VR_K(STACK, false, true, false, 3, 3, false, false, true);
+            else if (counting) VR_K(STACK, true, false, false, 3, 3, false, false, true);
+            else VR_K(STACK, false, false, false, 3, 3, false, false, true);
+        }
+        return launch_reduce(a, s, mid);
+    }
+    if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
+        if (recording) VR_K(STACK, false, true, true, 3, 3, true);
+        else if (counting) VR_K(STACK, true, false, true, 3, 3, true);
+        else VR_K(STACK, false, false, true, 3, 3, true);
+        return launch_reduce(a, s, mid);
+    }
+    // kinds present (bit 0 Lambertian, 1 reflective, 2 Phong or dielectric) -> specialisation:
+    // Lambertian-only (1), reflective-only (2) or the general kernel (3)
+    int mats = (c.mats == 1 || c.mats == 2) ? c.mats : 3;
+    if (!c.dark0) mats = 3;  // the general kernel
+#ifdef VR_TUNING_VARIANTS  // experiment hooks of tuning builds only (tools/variants.py)
+    // 1..4 = force that many waves per SIMD (default 3); VR_FORCE_MATS: the material specialisation
+    const char* ve = getenv("VR_KERNEL_VARIANT");
+    const int variant = ve ? atoi(ve) : 0;
+    if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);
+#define VR_MODES(D, M)                                          \
+    if (recording) VR_K(STACK, false, true, D, M, 3);           \
+    else if (counting) VR_K(STACK, true, false, D, M, 3);       \
+    else if (variant == 1) VR_K(STACK, false, false, D, M, 1);  \
+    else if (variant == 2) VR_K(STACK, false, false, D, M, 2);  \
+    else if (variant == 4) VR_K(STACK, false, false, D, M, 4);  \
+    else VR_K(STACK, false, false, D, M, 3)
+#else
+#define VR_MODES(D, M)                                    \
+    if (recording) VR_K(STACK, false, true, D, M, 3);     \
+    else if (counting) VR_K(STACK, true, false, D, M, 3); \
+    else VR_K(STACK, false, false, D, M, 3)
+#endif
+    // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
+    // of scenes with a reflective material)
+    const bool coop = c.coop;
+    if (!c.dark0) {
+        VR_MODES(false, 3);
+    } else if (mats == 1) {
+        VR_MODES(true, 1);
+    } else if (mats == 2) {
+        if (coop) VR_K(STACK, false, false, true, 2, 3, false, true);
+        else VR_MODES(true, 2);
+    } else {
+        if (coop) VR_K(STACK, false, false, true, 3, 3, false, true);
+        else VR_MODES(true, 3);
+    }
+#undef VR_MODES
+#undef VR_K
+    return launch_reduce(a, s, mid);
 }
 
 int launch_block_cull(const RenderArgs& a, uint8_t* mask, void* stream) {
@@ -1552,15 +1568,17 @@ int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32
     return (int)hipGetLastError();
 }
 
-int launch_render(const RenderArgs& a, int stack_depth, bool counting, bool recording, bool dark0, int mats,
-                  int grid_limit, void* stream, void* mid_event) {
+int launch_render(const RenderArgs& a, const LaunchChoice& c, int grid_limit, void* stream, void* mid_event) {
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t mid = (hipEvent_t)mid_event;
     if (a.tile_width == 0 || a.tile_height == 0 || a.spp == 0) return 0;
     hipError_t e;
-    if (stack_depth <= 24) e = launch_render_t<24>(a, counting, recording, dark0, mats, grid_limit, s, mid);
-    else if (stack_depth <= 32) e = launch_render_t<32>(a, counting, recording, dark0, mats, grid_limit, s, mid);
-    else if (stack_depth <= 48) e = launch_render_t<48>(a, counting, recording, dark0, mats, grid_limit, s, mid);
+    // the 64-bit-offset kernels exist in the deepest stack class only (a scene that needs them is
+    // far larger than any whose tree fits the smaller classes; more LDS is only fewer waves)
+    if (c.big && c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);
+    else if (c.stack_depth <= 24) e = launch_render_t<24>(a, c, grid_limit, s, mid);
+    else if (c.stack_depth <= 32) e = launch_render_t<32>(a, c, grid_limit, s, mid);
+    else if (c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);
     else return -1000;
     return (int)e;
 }

@@ -45,7 +45,7 @@ def reduce_bytes(state: torch.Tensor):
     return R.sums(state).numel() * state.element_size()
 
 
-def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None):
+def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None, keep_local=False):
     """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path).
 
     Only the merge-exact sums {sum X, sum Y, sum Z, weight} travel -- 32 B per pixel, the records'
@@ -54,8 +54,14 @@ def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None):
     (accumulation_buffer.rs:44-60), so `dst` zeroes them: an update_pixel continuation on the
     reduced state starts a fresh compensated sum from the merged totals.  On the other ranks the
     sums half belongs to the collective once called (in place: gloo uses it as scratch; the frame
-    is done with it), their compensations are untouched.  `timer`: a list that receives (start, end) CUDA events around everything this
-    call enqueues (the collective and the zeroing)."""
+    is done with it), their compensations are untouched.
+
+    So after the call a rank other than `dst` holds NO valid records: its sums half is collective
+    scratch, and an update_pixel continuation on it would silently build on garbage.  Callers that
+    keep accumulating on every rank pass `keep_local=True`: the collective then runs on a copy of
+    the sums half (32 B per pixel more HBM traffic), and the non-dst ranks' records stay their own.
+    `timer`: a list that receives (start, end) CUDA events around everything this call enqueues (the
+    collective and the zeroing)."""
     rank, world = world_info(group)
     # through the collective whenever a group exists (at world size 1 too: bench.py under
     # torch.distributed.run on one GPU rehearses the RCCL step the 8-GPU runs take)
@@ -66,7 +72,8 @@ def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None):
         if timer is not None and state.is_cuda:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        dist.reduce(sums, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        buf = sums.clone() if keep_local and rank != dst else sums
+        dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
         if rank == dst:
             R.compensations(flat).zero_()
         if ev is not None:
@@ -82,11 +89,13 @@ def mean_colour(state: torch.Tensor):
     return torch.where(w != 0, s[:, 0:3] * (1.0 / w), torch.zeros_like(s[:, 0:3]))
 
 
-def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=None):
+def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=None, keep_local=False):
     """One frame on this rank: render_shard(first_sample, state) renders (or enqueues) this rank's
     `spp` samples per pixel into `state` (fresh records), then the records are reduced onto rank 0.
-    Returns what render_shard returned (launch stats on the GPU)."""
+    Afterwards only rank 0's `state` is valid (the other ranks' sums half was the collective's
+    scratch) unless `keep_local` (reduce_records).  Returns what render_shard returned (launch stats
+    on the GPU)."""
     rank, world = world_info(group)
     out = render_shard(first_sample(step, rank, world, spp), state)
-    reduce_records(state, group=group, timer=timer)
+    reduce_records(state, group=group, timer=timer, keep_local=keep_local)
     return out

@@ -167,9 +167,20 @@ class AccumulationBuffer:
         return ImageRgbU8(out)
 
     @staticmethod
-    def from_state(state, width, height):
-        """Build from a tile's device-state records (vanrijn_amd/records.py layout)."""
-        f = R.fields(state, (height, width))
+    def from_state(state, width=None, height=None):
+        """Build from a tile's state records (vanrijn_amd/records.py layout, ABI 7: a flat array of
+        8 f64 per pixel, the sums half then the compensations half).  `width` / `height` may be left
+        out for a [height][width][8] array, whose shape gives them; such an array must hold the flat
+        layout reshaped, not the interleaved per-pixel records of ABI <= 6 -- a shape that does not
+        fit raises ValueError instead of misreading the data."""
+        a = np.asarray(state.cpu() if hasattr(state, "cpu") else state, dtype=np.float64)
+        if width is None or height is None:
+            if a.ndim != 3 or a.shape[2] != 8:
+                raise ValueError("from_state: pass width and height, or a [height][width][8] array")
+            height, width = a.shape[0], a.shape[1]
+        if a.size != 8 * width * height:
+            raise ValueError(f"from_state: {a.size} values for a {width}x{height} tile (8 f64 per pixel expected)")
+        f = R.fields(a.reshape(-1), (height, width))
         b = AccumulationBuffer(width, height)
         b.colour_sum_buffer[...] = f["colour_sum"]
         b.colour_bias_buffer[...] = f["colour_bias"]
@@ -235,16 +246,20 @@ def trace_rays(scene, origins, directions, device=0):
 
 
 def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample, state_ptr, stream_ptr=None,
-                       accumulate=False, timed=False, counters=False, device=0, defer_times=False, cull=True):
+                       accumulate=False, timed=False, counters=False, device=0, defer_times=False, cull=True,
+                       dist_cull=True, coop=True):
     """Enqueue a render into device state records (8 f64 per pixel, vanrijn_amd/records.py) at
     `state_ptr` (a device pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel
-    time when timed; `defer_times`: the events are recorded without waiting, read by
-    collect_launch_times; `cull=False`: every sample traced, VR_LAUNCH_NO_CULL)."""
+    time when timed; `variant`: the VR_VARIANT_* bits of the kernel that ran; `defer_times`: the
+    events are recorded without waiting, read by collect_launch_times; `cull=False`: every sample
+    traced, VR_LAUNCH_NO_CULL; `dist_cull=False`: no BVH distance culling, VR_LAUNCH_NO_DIST_CULL;
+    `coop=False`: no cooperative tail, VR_LAUNCH_NO_COOP -- all three leave the records bit-identical)."""
     ds = _scene_handle(scene, device)
     p = _params(tile, height, width, spp, seed, first_sample, accumulate)
     st = N.LaunchStats()
     flags = (N.LAUNCH_TIMED if timed or defer_times else 0) | (N.LAUNCH_COUNTERS if counters else 0) | \
-        (N.LAUNCH_DEFER_TIMES if defer_times else 0) | (0 if cull else N.LAUNCH_NO_CULL)
+        (N.LAUNCH_DEFER_TIMES if defer_times else 0) | (0 if cull else N.LAUNCH_NO_CULL) | \
+        (0 if dist_cull else N.LAUNCH_NO_DIST_CULL) | (0 if coop else N.LAUNCH_NO_COOP)
     N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
                                           C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
     return st.as_dict()
