@@ -107,6 +107,11 @@ OTHER_OPCODES = ["v_mov_b32", "v_xor_b32", "v_cndmask_b32_e64 (sgpr mask)", "v_c
                  "v_cmp_lt_f64", "v_max_f32", "v_max_f64", "v_min_f64", "v_div_scale_f64", "v_div_fixup_f64"]
 
 
+def progress(msg):
+    """A progress line on stderr (a long run shows it is alive; stdout carries only the JSON line)."""
+    print(f"bench.py [{time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def issue_costs():
     """Cycles per instruction per PMC class from the committed microbenchmark (None if absent)."""
     try:
@@ -241,6 +246,7 @@ def live_pmc(child_args, timeout_s=150):
             if rc != 0:
                 return {"error": f"PMC pass {name} exited {rc}"}
             c, ns = _fold_pass(d)
+            progress(f"PMC pass {name}: {', '.join(counters)}")
             for k in PMC_PASS_LOCAL.get(name, ()):
                 if k in c:
                     c[f"{k}@{name}"] = c.pop(k)
@@ -586,6 +592,7 @@ def main():
         step(1, timed=True)
         torch.cuda.synchronize()
         return
+    progress(f"scene built in {build_s:.3f} s; counting launch")
     # counting launch (untimed): traversal counters of exactly this workload
     counts = render_tile_device(dscene, tile, H, W, spp, SEED, rank * spp, state.data_ptr(), stream.cuda_stream,
                                 counters=True, device=local)
@@ -616,6 +623,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    progress(f"timed {args.steps} steps: {elapsed / args.steps * 1e3:.3f} ms/step")
     rccl_ms = [a.elapsed_time(b) for a, b in reduce_events]
     samples = world * args.steps * W * H * spp
     value = samples / elapsed / 1e6
@@ -666,10 +674,12 @@ def main():
     # (tests/test_gpu_cull.py); every sample is counted in `value`
     out["roofline"]["frustum_culled_sample_fraction"] = round(1.0 - counts["samples"] / (W * H * spp), 4)
     if rank == 0 and world == 1 and not args.no_drop_in:
+        progress("drop-in leg")
         out["drop_in"] = drop_in_leg(dscene, W, H, args.drop_in_frames, args.drop_in_threads, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ci = cpu_info()
         threads = args.cpu_threads or ci["usable"]
+        progress(f"CPU baseline on {threads} threads")
         out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds, threads)
         out["cpu_baseline"]["host"] = ci
     if rank == 0:
