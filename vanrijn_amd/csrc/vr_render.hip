@@ -135,6 +135,7 @@ __device__ __forceinline__ KArgs kargs() {
 }
 #define VR_NODES4 (kargs()->scene.nodes4)
 #define VR_TRIS (kargs()->scene.tris)
+#define VR_NODES4Q (kargs()->scene.nodes4q)
 
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
@@ -146,8 +147,10 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // BIG: 64-bit byte offsets for the node and triangle loads -- scenes whose triangle array reaches 4 GB
 // (53.7 M triangles) or whose 4-wide tree has 2^25 nodes (vr_host.cpp needs_big_offsets); every other
 // scene's kernels address both arrays with 32-bit offsets from the scalar base (the loads' saddr form)
+// QNODE: the node step reads the 64-B quantised nodes (Node4q, vr_qnode.h) instead of the 128-B
+// Node4 -- large trees, whose traversal is bound by L2 misses (C5); never with COOP
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          bool COOP = false, bool BIG = false>
+          bool COOP = false, bool BIG = false, bool QNODE = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -250,6 +253,10 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     auto node_at = [&](int n) -> const Node4& {
         if (BIG) return VR_NODES4[(uint32_t)n];
         return *(const Node4*)((const char*)VR_NODES4 + ((uint32_t)n << 7));
+    };
+    auto qnode_at = [&](int n) -> const Node4q* {
+        if (BIG) return VR_NODES4Q + (uint32_t)n;
+        return (const Node4q*)((const char*)VR_NODES4Q + ((uint32_t)n << 6));
     };
     auto takes_hit = [&](double d, uint32_t rk) {
         const bool closer = !best.kind | (d < best.d);
@@ -1022,7 +1029,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 VR_MARK("node_step");
                 // 32-bit byte offset from the scalar base (node < 2^25 unless BIG): the load's saddr form,
                 // no 64-bit address arithmetic per step
-                const Node4& nd = node_at(node);
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
@@ -1033,17 +1039,35 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 // test runs in the leaf round, beside the triangle test (the f32 bounds tlo / thi
                 // enclose the exact interval either way, so the f32 cull stays conservative)
                 uint32_t hm = 0, xm = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    c[k] = nd.child[k];
-                    float g;
-                    bool maybe, sure;
-                    slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
+                auto child_flags = [&](int k, float g, bool maybe, bool sure) {
                     const bool live = c[k] != kEmptyChild;
                     if (COUNT && live) cnt.box_tests++;
                     const bool pass = live && maybe && !(f[k] > cull_far || g < cull_behind);
                     hm |= pass ? 1u << k : 0u;
                     xm |= (pass && !sure) ? 1u << k : 0u;
+                };
+                if constexpr (QNODE) {
+                    // the quantised node: one 64-B record, the grid's slab constants once per node
+                    const Node4q nq = load_node4q(qnode_at(node));
+                    const QFrame qf = qframe(nq, pre32);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        c[k] = nq.child[k];
+                        float g;
+                        bool maybe, sure;
+                        slab32q_flags(nq, k, qf, pre32, f[k], g, maybe, sure);
+                        child_flags(k, g, maybe, sure);
+                    }
+                } else {
+                    const Node4& nd = node_at(node);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        c[k] = nd.child[k];
+                        float g;
+                        bool maybe, sure;
+                        slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
+                        child_flags(k, g, maybe, sure);
+                    }
                 }
                 // leaf children: their triangles go to the wave FIFO, appended after the step by all
                 // lanes at once
@@ -1508,6 +1532,22 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
         }
         return launch_reduce(a, s, mid);
     }
+    if (c.qnode) {
+        // quantised nodes (large trees): the Lambertian-only DARK0 kernels (C5) and the general
+        // ones, in the stack classes 32 and 48 only (launch_render)
+        if constexpr (STACK < 32) return hipErrorInvalidValue;
+        else if (a.scene.integrator == 1) return hipErrorInvalidValue;  // (never chosen: vr_host.cpp)
+        else if (c.dark0 && c.mats == 1) {
+            if (recording) VR_K(STACK, false, true, true, 1, 3, false, false, false, true);
+            else if (counting) VR_K(STACK, true, false, true, 1, 3, false, false, false, true);
+            else VR_K(STACK, false, false, true, 1, 3, false, false, false, true);
+        } else {
+            if (recording) VR_K(STACK, false, true, false, 3, 3, false, false, false, true);
+            else if (counting) VR_K(STACK, true, false, false, 3, 3, false, false, false, true);
+            else VR_K(STACK, false, false, false, 3, 3, false, false, false, true);
+        }
+        return launch_reduce(a, s, mid);
+    }
     if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
         if (recording) VR_K(STACK, false, true, true, 3, 3, true);
         else if (counting) VR_K(STACK, true, false, true, 3, 3, true);
@@ -1576,6 +1616,7 @@ int launch_render(const RenderArgs& a, const LaunchChoice& c, int grid_limit, vo
     // the 64-bit-offset kernels exist in the deepest stack class only (a scene that needs them is
     // far larger than any whose tree fits the smaller classes; more LDS is only fewer waves)
     if (c.big && c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);
+    else if (c.qnode && c.stack_depth <= 32) e = launch_render_t<32>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 24) e = launch_render_t<24>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 32) e = launch_render_t<32>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);
