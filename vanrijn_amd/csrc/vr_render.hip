@@ -116,6 +116,9 @@ constexpr int kPrioA = 0, kPrioNode = 1, kPrioLeaf = 1;
 #ifndef VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
 #define VR_WATCHDOG 0
 #endif
+#ifndef VR_COOP_SORT  // the cooperative tail pushes its frontier near-first (coop_step)
+#define VR_COOP_SORT 1
+#endif
 constexpr int kPend = 8;  // FIFO entries per lane of a wave, on average
 constexpr int kWaveList = 64 * kPend;
 static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
@@ -736,6 +739,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         const bool work = t > 0 && VR_ROOM;  // uniform per half
         uint32_t im = 0;                     // hit interior children
         int c[4] = {0, 0, 0, 0};
+        float fk[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // their f32 entry distances
         int pos = o_sp;
         if (work) {
             VR_MARK("coop_step");
@@ -769,6 +773,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     const bool lv = c[k] != kEmptyChild;
                     if (COUNT && lv) cnt.box_tests++;
                     const bool pass = lv && maybe && !(f > cf || g < cb);
+                    fk[k] = f;
                     xm |= (pass && !sure) ? 1u << k : 0u;
                     im |= (pass && c[k] >= 0) ? 1u << k : 0u;
                     lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
@@ -776,6 +781,69 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
             }
         }
+#if VR_COOP_SORT
+        // interior hits onto the owner's stack near-first: the owner pops the top, so
+        // the walk follows the nearest child found in the step as the per-lane walk does.  Each
+        // worker orders its hit children by packed key (the node step's: the entry distance's bits
+        // over the child index, A.sort_mask); the workers are ordered, across the owner's lanes, by
+        // their nearest key, farthest first (a bitonic network of lane shuffles on one 64-bit key per
+        // lane: nearest key << 32 | worker); every worker writes its children farthest-first from
+        // its place in that order.  Top of stack: the step's nearest child; below it the rest of its
+        // worker's, then the next-nearest worker's.  Only the visiting order changes (DESIGN.md
+        // section 5: the closest hit and its tie rule do not depend on it).
+        {
+            const uint32_t smask = A.sort_mask;
+            uint32_t key[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool h = (im >> k) & 1u;
+                key[k] = h ? (((uint32_t)max(__float_as_int(fk[k]), 0) & ~smask) | (uint32_t)c[k]) : 0xffffffffu;
+            }
+            auto cas = [&](int i, int j) {
+                const uint32_t ki = key[i], kj = key[j];
+                key[i] = ki < kj ? ki : kj;
+                key[j] = ki < kj ? kj : ki;
+            };
+            cas(0, 1);
+            cas(2, 3);
+            cas(0, 2);
+            cas(1, 3);
+            cas(1, 2);  // ascending: key[0] the worker's nearest
+            const int nh = (int)__popc(im);
+            // one record per lane of the group, sorted DESCENDING by (nearest key, worker rank): the
+            // worker with no hit (key 0xffffffff) sorts first and pushes nothing
+            uint64_t rec = ((uint64_t)key[0] << 32) | (uint32_t)r;
+            for (int kk = 2; kk <= gsize; kk <<= 1) {
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(rec >> 32), j) << 32) |
+                                       (uint32_t)__shfl_xor((int)(uint32_t)rec, j);
+                    const bool lower = (r & j) == 0, desc = (r & kk) == 0;
+                    // descending blocks keep the larger record in the lower lane
+                    const bool keep_max = lower == desc;
+                    rec = keep_max ? (rec > o ? rec : o) : (rec < o ? rec : o);
+                }
+            }
+            // position r of the order holds worker w = rec's low half; its pushes start after the
+            // pushes of positions < r: an exclusive prefix sum of the workers' hit counts in order
+            const int w = (int)(uint32_t)rec;
+            int cntw = __shfl(nh, gbase + w);
+            int incl = cntw;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                if (d >= gsize) break;
+                const int v = __shfl_up(incl, (unsigned)d, gsize);
+                if (r >= d) incl += v;
+            }
+            const int excl = incl - cntw;
+            // hand each worker its start: lane gbase + r sends `excl` to lane gbase + w
+            const int start = __builtin_amdgcn_ds_permute((gbase + w) << 2, excl);
+            // farthest first: key[nh - 1] lowest, key[0] on top
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < nh) st_node[coop_vaddr(owner, om, pos + start + (nh - 1 - k))] = key[k] & smask;
+            pos += __shfl(incl, gbase + gsize - 1);  // all the group's pushes
+        }
+#else
         // interior hits onto the owner's stack, in (child slot, worker) order
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -784,6 +852,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (ih) st_node[coop_vaddr(owner, om, pos + (int)lanes_below(m))] = (uint32_t)c[k];
             pos += (int)__popcll(m);
         }
+#endif
         // each owner takes its next node, the top of its stack: its workers' pos and work flag
         // (uniform over its half) by permute from the half's first lane
         const int lead = (two && (int)lane == ob) ? 32 : 0;
