@@ -515,9 +515,6 @@ def main():
     ap.add_argument("--drop-in-threads", type=int, default=8)
     ap.add_argument("--no-drop-in", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes of the roofline")
-    ap.add_argument("--nodes", choices=["auto", "full", "quantized"], default="auto",
-                    help="the 4-wide tree's node records: 64-B quantised for trees of >= 131,072 nodes (auto), or "
-                         "forced (A/B; the same images)")
     ap.add_argument("--host-build", action="store_true",
                     help="render the host-built traversal tree instead of the device-built one (same images)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
@@ -565,15 +562,14 @@ def main():
     # scene every timed step renders; and, for comparison, the same scene built on the host
     torch.cuda.synchronize()
     t_build = time.perf_counter()
-    qn = {"auto": None, "full": False, "quantized": True}[args.nodes]
-    dscene = scene.device_scene(local, device_sah=not args.host_build, quantized_nodes=qn)
+    dscene = scene.device_scene(local, device_sah=not args.host_build)
     info = dscene.info()
     build_s = time.perf_counter() - t_build
     build = {"rendered_tree": "host-built" if args.host_build else "device-built (VR_SCENE_DEVICE_SAH)",
              "seconds": round(build_s, 4)}
     if not args.pmc_child:
         t_build = time.perf_counter()
-        scene.device_scene(local, device_sah=args.host_build, quantized_nodes=qn).info()
+        scene.device_scene(local, device_sah=args.host_build).info()
         build["other_build_seconds"] = round(time.perf_counter() - t_build, 4)
         build["other_build"] = "device-built (VR_SCENE_DEVICE_SAH)" if args.host_build else \
             "host-built (median ranks + binned SAH + 4-wide on the CPU)"
@@ -656,14 +652,13 @@ def main():
                 f"{os.path.basename(args.mesh)} (sha256-verified reference bunny), counter-based RNG seed 0x5EED0001",
         "config": {"workload": workload, "config": args.config, "width": W, "height": H, "spp_per_gpu": spp,
                    "triangles": info["triangle_count"], "bvh_depth": info["max_bvh_depth"],
-                   "wide_nodes": info["wide_node_count"], "quantized_nodes": info["quantized_nodes"],
                    "parallelism": f"spp-split x{world}, RCCL reduce",
                    "pmc_key": config_key(cfg["scene"], W, H, spp)},
     }
     pmc = None
     if rank == 0 and world == 1 and not args.no_pmc:
         child = ["--config", args.config, "--width", str(W), "--height", str(H), "--spp", str(cfg["spp"]),
-                 "--scene", cfg["scene"], "--nodes", args.nodes] + (["--mesh", args.mesh] if args.mesh else []) + \
+                 "--scene", cfg["scene"]] + (["--mesh", args.mesh] if args.mesh else []) + \
                 (["--host-build"] if args.host_build else [])
         pmc = live_pmc(child)
     out["roofline"] = roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes), pmc)

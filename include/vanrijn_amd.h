@@ -176,12 +176,6 @@ typedef struct vr_scene vr_scene;
  * records (53.7 M triangles) or 2^25 nodes of the 4-wide tree (vr_scene_needs_wide_offsets); this
  * flag exercises them on small scenes (tests).  Renders are identical either way. */
 #define VR_SCENE_WIDE_OFFSETS 32u
-/* The render kernel's 4-wide tree in 64 B per node: child boxes quantised to 8 bits per plane on a
- * per-node grid, rounded outward (ABI 8).  By default a scene gets it when its
- * 4-wide tree has at least 131,072 nodes (trees that overflow the L2, like C5's); these flags force
- * it on or off.  Renders are identical either way (VR_SCENE_INFO_QUANTIZED_NODES reports the choice). */
-#define VR_SCENE_QUANTIZED_NODES 64u
-#define VR_SCENE_FULL_NODES 128u
 
 /* Replaces building `Scene { camera_location, objects }` + BoundingVolumeHierarchy::build.
  * Copies every input; builds one BVH per mesh with the reference's median split
@@ -208,7 +202,6 @@ typedef struct vr_scene_info {
  * mesh.rs:37 gives an OBJ without normals) reaches the pixel as the reference's 0 * NaN does
  * (simple_random_integrator.rs:39-53). */
 #define VR_SCENE_INFO_NAN_FREE 1u
-#define VR_SCENE_INFO_QUANTIZED_NODES 2u /* the render kernel walks the 64-B quantised nodes (ABI 8) */
 int vr_scene_get_info(const vr_scene* scene, vr_scene_info* out);
 /* BVH leaf (in-order) sequence of mesh `mesh`: out[i] = input triangle index of leaf i. */
 int vr_scene_bvh_leaf_order(const vr_scene* scene, uint32_t mesh, uint64_t* out);
@@ -285,7 +278,6 @@ typedef struct vr_launch_stats {
 } vr_launch_stats;
 #define VR_VARIANT_COOP 1u         /* the cooperative-tail instantiation (small launches, mirror scenes) */
 #define VR_VARIANT_WIDE_OFFSETS 2u /* the 64-bit-offset kernels (VR_SCENE_WIDE_OFFSETS) */
-#define VR_VARIANT_QUANTIZED_NODES 4u /* the node step read the 64-B quantised nodes */
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */
 #define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
@@ -304,9 +296,6 @@ typedef struct vr_launch_stats {
 /* no cooperative tail (small launches of scenes with a reflective material otherwise spread a
  * wave's last one or two paths over its lanes): the same records bit for bit (ABI 8) */
 #define VR_LAUNCH_NO_COOP 32u
-/* a scene with quantised nodes walks its 128-B nodes in this launch (A/B measurements; the same
- * records bit for bit; ABI 8) */
-#define VR_LAUNCH_FULL_NODES 64u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
@@ -410,10 +399,6 @@ int vr_debug_set_launch_flags(vr_scene* scene, uint32_t flags);
 /* 1 when a scene with this many triangles and 4-wide nodes renders with the 64-bit-offset kernels
  * (VR_SCENE_WIDE_OFFSETS), else 0.  Host only, no device (ABI 8). */
 int vr_scene_needs_wide_offsets(uint64_t triangle_count, uint64_t wide_node_count);
-/* The quantiser of VR_SCENE_QUANTIZED_NODES on the host, for the CPU soundness test: a 4-wide node's
- * f32 child boxes (4 x {min x, max x, min y, max y, min z, max z}) and links -> its 64-B quantised
- * record (vr_qnode.h layout) in out64.  VR_ERROR_INVALID_ARGUMENT for a non-finite live box (ABI 8). */
-int vr_quantize_wide_node(const float boxes[24], const int32_t children[4], void* out64);
 
 int vr_device_count(void);
 const char* vr_last_error(void);

@@ -135,52 +135,3 @@ def test_wide_offset_kernels_are_bit_identical(which):
         out.append((st.cpu(), rec, c["node_visits"]))
     assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))  # bitwise, NaN included
     assert out[0][1].tobytes() == out[1][1].tobytes()
-
-
-@pytest.mark.parametrize("which", ["main", "bench"])
-def test_quantised_nodes_are_bit_identical(which):
-    """The 64-B quantised 4-wide nodes (forced on a small tree) render the records of the 128-B ones
-    -- timed, counting and per-sample record instantiations -- and the launch reports which ran."""
-    scene = {"main": scenes.main_scene, "bench": scenes.bench_scene}[which]()
-    H, W = 160, 200
-    t = Tile(10, 190, 20, 150)
-    npix = t.width() * t.height()
-    out = []
-    for q in (False, True):
-        ds = DeviceScene(scene.spec(), 0, device_sah=True, quantized_nodes=q)
-        assert ds.info()["quantized_nodes"] == q
-        st = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
-        s = render_tile_device(ds, t, H, W, 6, 0x5EED0001, 0, st.data_ptr())
-        c = render_tile_device(ds, t, H, W, 2, 0x5EED0001, 6, st.data_ptr(), accumulate=True, counters=True)
-        torch.cuda.synchronize()
-        assert bool(s["variant"] & N.VARIANT_QUANTIZED_NODES) == q
-        assert bool(c["variant"] & N.VARIANT_QUANTIZED_NODES) == q
-        rec = render_samples(ds, t, H, W, 2, seed=0x5EED0001)
-        out.append((st.cpu(), rec, c))
-    assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))
-    assert out[0][1].tobytes() == out[1][1].tobytes()
-    print(f"{which}: node visits full {out[0][2]['node_visits']} quantised {out[1][2]['node_visits']}, "
-          f"exact box tests {out[0][2]['exact_box_tests']} / {out[1][2]['exact_box_tests']}")
-
-
-def test_c5_mesh_takes_quantised_nodes(oracle):
-    """C5's 1,051,392-triangle mesh (413 K wide nodes) gets the quantised nodes by default: a crop
-    renders the 128-B nodes' records bit for bit (VR_LAUNCH_FULL_NODES) and the oracle's image."""
-    scene = scenes.synthetic_scene()
-    ds = scene.device_scene(0, device_sah=True)
-    assert ds.info()["quantized_nodes"]
-    H = W = 4096
-    t = Tile(1700, 1764, 2200, 2264)  # test_gpu_parity_configs.py C5 crop (> 10 K camera hits)
-    npix = t.width() * t.height()
-    a = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
-    b = torch.zeros_like(a)
-    sa = render_tile_device(ds, t, H, W, 4, 0x5EED0001, 0, a.data_ptr())
-    sb = render_tile_device(ds, t, H, W, 4, 0x5EED0001, 0, b.data_ptr(), full_nodes=True)
-    torch.cuda.synchronize()
-    assert sa["variant"] & N.VARIANT_QUANTIZED_NODES and not sb["variant"] & N.VARIANT_QUANTIZED_NODES
-    assert torch.equal(a.view(torch.int64), b.view(torch.int64))
-    img = render_tile(ds, t, H, W, 4, seed=0x5EED0001)
-    ref = oracle.OracleScene(scene.spec()).render_tile(t, H, W, 4, seed=0x5EED0001, mode=oracle.MODE_PRUNED,
-                                                       nthreads=8)
-    assert np.linalg.norm(img.colour_buffer - ref["colour"], axis=2).max() < 1e-5
-    assert np.array_equal(img.weight_buffer, ref["weight"])

@@ -15,10 +15,9 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the C3 timed kernel: STACK 32, Lambertian-only, DARK0, no Whitted, no cooperative tail (VR_ISA_STACK /
-# VR_ISA_MATS / VR_ISA_COOP=1 / VR_ISA_QNODE=1 pick another instantiation)
-KERNEL = ("_ZN2vr3dev13render_kernelILi%sELb0ELb0ELb1ELi%sELi3ELb0ELb%sELb0ELb%sEEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
-          % (os.environ.get("VR_ISA_STACK", "32"), os.environ.get("VR_ISA_MATS", "1"), os.environ.get("VR_ISA_COOP", "0"),
-             os.environ.get("VR_ISA_QNODE", "0")))
+# VR_ISA_MATS / VR_ISA_COOP=1 pick another instantiation)
+KERNEL = ("_ZN2vr3dev13render_kernelILi%sELb0ELb0ELb1ELi%sELi3ELb0ELb%sELb0EEEvNS_10RenderArgsEPKNS_4PrimEPKNS_8MaterialEPKNS_3BvhE"
+          % (os.environ.get("VR_ISA_STACK", "32"), os.environ.get("VR_ISA_MATS", "1"), os.environ.get("VR_ISA_COOP", "0")))
 
 
 def cost(op):

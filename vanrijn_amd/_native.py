@@ -25,11 +25,10 @@ SCENE_REFERENCE_BVH = 4
 SCENE_DEVICE_SAH = 8
 SCENE_GREEDY_COLLAPSE = 16
 SCENE_WIDE_OFFSETS = 32
-SCENE_QUANTIZED_NODES, SCENE_FULL_NODES = 64, 128
 LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES, LAUNCH_NO_CULL = 1, 2, 4, 8
-LAUNCH_NO_DIST_CULL, LAUNCH_NO_COOP, LAUNCH_FULL_NODES = 16, 32, 64
-VARIANT_COOP, VARIANT_WIDE_OFFSETS, VARIANT_QUANTIZED_NODES = 1, 2, 4
-SCENE_INFO_NAN_FREE, SCENE_INFO_QUANTIZED_NODES = 1, 2
+LAUNCH_NO_DIST_CULL, LAUNCH_NO_COOP = 16, 32
+VARIANT_COOP, VARIANT_WIDE_OFFSETS = 1, 2
+SCENE_INFO_NAN_FREE = 1
 
 
 class VrError(RuntimeError):
@@ -167,7 +166,6 @@ SIGNATURES = {
     "vr_debug_set_fault_object": (C.c_int, [_p, _i32]),
     "vr_debug_set_launch_flags": (C.c_int, [_p, _u32]),
     "vr_scene_needs_wide_offsets": (C.c_int, [_u64, _u64]),
-    "vr_quantize_wide_node": (C.c_int, [_p, _p, _p]),
     "vr_device_count": (C.c_int, []),
     "vr_last_error": (C.c_char_p, []),
     "vr_abi_version": (C.c_uint32, []),

@@ -34,7 +34,6 @@
 #include <vector>
 
 #include "vr_layout.h"
-#include "vr_qnode.h"
 
 namespace vr {
 namespace build {
@@ -667,22 +666,6 @@ int device_build_sah(TriVerts* tris, TriNormals* normals, uint32_t n, int32_t no
     if (c[1] != n - 1) return (int)hipErrorUnknown;  // every interior node allocated exactly once
     *levels = (int)c[2];
     return 0;
-}
-
-// Node4 -> Node4q (vr_qnode.h), one thread per wide node; *bad counts nodes whose boxes are not finite
-__global__ void quantize_wide_kernel(const Node4* in, uint64_t n, Node4q* out, unsigned int* bad) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    Node4q q;
-    if (!quantize_node4(in[i], q)) atomicAdd(bad, 1u);
-    out[i] = q;
-}
-
-int device_quantize_wide(const Node4* in, uint64_t n, Node4q* out, unsigned int* bad, void* stream) {
-    if (n == 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(quantize_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out, bad);
-    return (int)hipGetLastError();
 }
 
 int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream) {

@@ -433,61 +433,6 @@ __device__ __forceinline__ void slab32_flags(const float* b, const Ray32& r, flo
     maybe = !(d > r.e2);
 }
 
-// Quantised 4-wide nodes (Node4q, vr_qnode.h).  Per node and ray: the grid step in slab units
-// S_a = 2^exp_a * i_a (exact: i_a is a normal f32 >= 1 in magnitude for a unit direction) and the
-// slab value of the grid's corner c_a = fma(origin_a, i_a, -(o_a i_a)) -- the plane-at-origin
-// value slab32 would compute.  A plane's value is then t = fma(q, S_a, c_a).  Error against the
-// exact (origin + q 2^e - o) / d: c's 2.4e-7 |c| + 1.2e-7 |o| m <= 6e-7 X m (|c| <= 2 X m), the
-// reciprocal's 1.8e-7 on q 2^e / d (<= 2 X m), the fma's 6e-8 |t| (|t| <= 4 X m): 1.2e-6 X m per
-// value, so a difference lo - hi within 2.4e-6 X m of the exact one -- inside the per-ray 2E = 3.6e-6
-// X m the f32 tests use (vr_device.h Ray32), and each value within E (1.8e-6 X m) for the cull
-// thresholds.  tests/test_qnode.py checks this on the CPU.
-//   maybe: !(lo - hi > 2E) on the decoded (outer) box, which contains the child's f64 box;
-//   sure:  lo - hi < -(2E + 2 dq): the box shrunk by one grid step per side -- inside the child's
-//          f64 box up to the f32 rounding E already budgets -- passes; dq = max_a |S_a| bounds the
-//          step's effect on lo and hi (widened by 2^-20 for the reciprocal's rounding).
-struct QFrame {
-    float sx, sy, sz;  // S_a
-    float cx, cy, cz;  // c_a
-    float sure_thr;    // -(2E + 2 dq), rounded away from 0
-};
-__device__ __forceinline__ Node4q load_node4q(const Node4q* p) {
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    const u4* q = reinterpret_cast<const u4*>(p);
-    u4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-    const u4 w[4] = {w0, w1, w2, w3};
-    Node4q n;
-    __builtin_memcpy(&n, w, sizeof n);
-    return n;
-}
-__device__ __forceinline__ QFrame qframe(const Node4q& n, const Ray32& r) {
-    QFrame f;
-    f.sx = ldexpf(r.ix, n.exp[0]);
-    f.sy = ldexpf(r.iy, n.exp[1]);
-    f.sz = ldexpf(r.iz, n.exp[2]);
-    f.cx = __builtin_fmaf(n.origin[0], r.ix, r.nx);
-    f.cy = __builtin_fmaf(n.origin[1], r.iy, r.ny);
-    f.cz = __builtin_fmaf(n.origin[2], r.iz, r.nz);
-    const float dq = fmaxf(fmaxf(fabsf(f.sx), fabsf(f.sy)), fabsf(f.sz));
-    f.sure_thr = -((r.e2 + dq * 2.000002f) * (1.0f + 0x1p-22f));
-    return f;
-}
-// child k's decoded slab: lo / hi as slab32_flags, `maybe` on the outer box, `sure` on the inner one
-// (k a constant after unrolling: the byte extract and conversion become one v_cvt_f32_ubyte<k>)
-__device__ __forceinline__ void slab32q_flags(const Node4q& n, int k, const QFrame& f, const Ray32& r, float& lo,
-                                              float& hi, bool& maybe, bool& sure) {
-    auto qv = [&](int j) { return (float)((n.q[j] >> (8 * k)) & 0xffu); };
-    const vr_f2 tx = __builtin_elementwise_fma((vr_f2){qv(0), qv(1)}, (vr_f2){f.sx, f.sx}, (vr_f2){f.cx, f.cx});
-    const vr_f2 ty = __builtin_elementwise_fma((vr_f2){qv(2), qv(3)}, (vr_f2){f.sy, f.sy}, (vr_f2){f.cy, f.cy});
-    const vr_f2 tz = __builtin_elementwise_fma((vr_f2){qv(4), qv(5)}, (vr_f2){f.sz, f.sz}, (vr_f2){f.cz, f.cz});
-    lo = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-    hi = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const float d = lo - hi;
-    sure = d < f.sure_thr;
-    maybe = !(d > r.e2);
-}
-
 // A triangle record in one batch of five dwordx4 loads.  Left to itself the scheduler issued the
 // last vertex's z only after the first four loads had returned (two memory round trips per
 // triangle test); the empty asm needs all five values at once, so all five are in flight together.

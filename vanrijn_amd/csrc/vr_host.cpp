@@ -34,7 +34,6 @@
 #include "../../include/vanrijn_amd.h"
 #include "rgb_spectrum_tables.h"
 #include "vr_layout.h"
-#include "vr_qnode.h"
 
 #include <zlib.h>
 
@@ -540,9 +539,6 @@ struct vr_scene {
     bool device_sah = false;  // VR_SCENE_DEVICE_SAH: the SAH traversal tree too (vr_build.hip)
     bool greedy_collapse = false;  // VR_SCENE_GREEDY_COLLAPSE: the 4-wide tree by largest child area
     bool force_big = false;        // VR_SCENE_WIDE_OFFSETS: the 64-bit-offset kernels for any size
-    int qnode_mode = 0;            // VR_SCENE_QUANTIZED_NODES: 1 (on), VR_SCENE_FULL_NODES: -1 (off), 0: by size
-    bool quantized = false;        // the render kernel reads the 64-B quantised nodes (dev.nodes4q)
-    void* d_qnodes = nullptr;      // their device array (wide_count x 64 B)
     uint64_t staging_limit = 0;    // vr_scene_set_staging_limit: bytes of staging per call (0: half the free HBM)
     uint64_t node_count = 0, tri_count = 0;
     struct PendingMesh {
@@ -983,36 +979,6 @@ int upload(vr_scene* s) {
     return VR_OK;
 }
 
-// The 64-B quantised copy of the 4-wide tree (vr_qnode.h) for trees of at least kQuantizeMinNodes
-// wide nodes -- their traversal misses L2 (C5: hit rate 0.56); smaller trees stay L2-resident and
-// keep the 128-B nodes, whose test needs no decoding -- or as the scene flags force.  Scenes whose
-// wide nodes hold a non-finite box, Whitted scenes (their kernels have no quantised variant) and
-// scenes past the 32-bit load offsets keep the 128-B nodes.
-constexpr uint64_t kQuantizeMinNodes = 131072;
-int quantize_nodes(vr_scene* s) {
-    s->dev.nodes4q = nullptr;
-    s->quantized = false;
-    const bool want = s->qnode_mode > 0 || (s->qnode_mode == 0 && s->wide_count >= kQuantizeMinNodes);
-    if (!want || s->wide_count == 0 || s->dev.integrator == 1 || needs_big_offsets(s)) return VR_OK;
-    VR_HIP(hipSetDevice(s->device));
-    VR_HIP(hipMalloc(&s->d_qnodes, s->wide_count * sizeof(vr::Node4q) + 256));
-    unsigned int* d_bad = (unsigned int*)((char*)s->d_qnodes + s->wide_count * sizeof(vr::Node4q));
-    VR_HIP(hipMemset(d_bad, 0, sizeof(unsigned int)));
-    const int e = vr::device_quantize_wide(s->dev.nodes4, s->wide_count, (vr::Node4q*)s->d_qnodes, d_bad, nullptr);
-    if (e) return fail(VR_ERROR_DEVICE, std::string("node quantisation failed: ") + hipGetErrorString((hipError_t)e));
-    unsigned int bad = 0;
-    VR_HIP(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
-    if (bad) {  // a non-finite box: the 128-B nodes only
-        VR_HIP(hipFree(s->d_qnodes));
-        s->d_qnodes = nullptr;
-        return VR_OK;
-    }
-    s->dev.nodes4q = (const vr::Node4q*)s->d_qnodes;
-    s->quantized = true;
-    s->device_bytes += s->wide_count * sizeof(vr::Node4q);
-    return VR_OK;
-}
-
 int check_render_params(const vr_scene* s, const vr_render_params* p) {
     if (!s || !p) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene or params");
     if (s->host_only) return fail(VR_ERROR_HOST_ONLY, "scene was created with VR_SCENE_HOST_ONLY");
@@ -1355,7 +1321,6 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     s->host_only = (flags & VR_SCENE_HOST_ONLY) != 0;
     s->greedy_collapse = (flags & VR_SCENE_GREEDY_COLLAPSE) != 0;
     s->force_big = (flags & VR_SCENE_WIDE_OFFSETS) != 0;
-    s->qnode_mode = (flags & VR_SCENE_QUANTIZED_NODES) ? 1 : ((flags & VR_SCENE_FULL_NODES) ? -1 : 0);
     s->camera[0] = desc->camera_location.x;
     s->camera[1] = desc->camera_location.y;
     s->camera[2] = desc->camera_location.z;
@@ -1626,7 +1591,6 @@ int vr_scene_create(const vr_scene_desc* desc, int32_t device, uint32_t flags, v
     d.extent = extent;
     if (!s->host_only) {
         int rc = upload(s);
-        if (rc == VR_OK) rc = quantize_nodes(s);
         if (rc != VR_OK) {
             std::string msg = g_last_error;
             vr_scene_destroy(s);
@@ -1645,7 +1609,6 @@ void vr_scene_destroy(vr_scene* s) {
         // (the streams may be gone by now: hipFree waits for the device instead)
         for (auto& kv : s->stream_slots) (void)hipFree(kv.second);
         if (s->d_block) (void)hipFree(s->d_block);
-        if (s->d_qnodes) (void)hipFree(s->d_qnodes);
     }
     for (auto& kv : s->deferred)
         for (hipEvent_t e : kv.second.ev) (void)hipEventDestroy(e);
@@ -1662,7 +1625,7 @@ int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
     out->device_bytes = s->device_bytes;
     out->wide_node_count = s->wide_count;
     out->traversal_stack = (uint32_t)s->wide_stack;
-    out->flags = (s->nan_free ? VR_SCENE_INFO_NAN_FREE : 0u) | (s->quantized ? VR_SCENE_INFO_QUANTIZED_NODES : 0u);
+    out->flags = s->nan_free ? VR_SCENE_INFO_NAN_FREE : 0u;
     return VR_OK;
 }
 
@@ -1680,21 +1643,9 @@ int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
 
 int vr_debug_set_launch_flags(vr_scene* s, uint32_t flags) {
     if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
-    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP | VR_LAUNCH_FULL_NODES;
-    if (flags & ~allowed)
-        return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP / FULL_NODES apply to every call");
+    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP;
+    if (flags & ~allowed) return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP apply to every call");
     s->debug_launch_flags = flags;
-    return VR_OK;
-}
-
-int vr_quantize_wide_node(const float boxes[24], const int32_t children[4], void* out64) {
-    if (!boxes || !children || !out64) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
-    vr::Node4 w;
-    std::memcpy(w.box, boxes, sizeof w.box);
-    std::memcpy(w.child, children, sizeof w.child);
-    vr::Node4q q;
-    if (!vr::quantize_node4(w, q)) return fail(VR_ERROR_INVALID_ARGUMENT, "a live child's box is not finite");
-    std::memcpy(out64, &q, sizeof q);
     return VR_OK;
 }
 
@@ -1857,14 +1808,10 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         lc.dark0 = s->dark0;
         lc.mats = s->mats ? s->mats : 3;
         lc.big = needs_big_offsets(s);
-        lc.qnode = s->quantized && !lc.big && !(launch_flags & VR_LAUNCH_FULL_NODES);
         // the cooperative tail's instantiations exist for DARK0 scenes with a reflective material
         lc.coop = a.coop != 0 && !recording && !counting && !lc.big && s->dev.integrator != 1 && s->dark0 &&
                   (lc.mats & 2);
-        if (lc.qnode) lc.coop = false;  // (the cooperative tail walks the 128-B nodes)
-        if (variant)
-            *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u) |
-                       (lc.qnode ? VR_VARIANT_QUANTIZED_NODES : 0u);
+        if (variant) *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u);
         int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * grid_per_cu(), st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {

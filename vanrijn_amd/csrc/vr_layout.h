@@ -44,24 +44,6 @@ struct alignas(128) Node4 {
 };
 static_assert(sizeof(Node4) == 128, "Node4 must be one 128-B line");
 
-// The same 4-wide node in 64 B (round 5; large trees, vr_host.cpp use_quantized_nodes): child boxes
-// quantised to 8 bits per plane on a per-node grid, two nodes per 128-B line.  Plane j of child k
-// is the real number origin[a] + q[j][k] * 2^exp[a] (a = j / 2; j even: lower plane, odd: upper),
-// rounded OUTWARD from the child's f32 box (vr_qnode.h quantize_node4): every decoded box contains
-// its Node4 box, hence its f64 box -- an interior child is a superset as before (DESIGN.md
-// section 5), and a leaf child is "surely hit" only when the decoded box shrunk by one grid step
-// per side (inside the true box) passes.  q is stored plane-major, one dword per plane with the
-// four children in its bytes (v_cvt_f32_ubyte<k> decodes child k's value).
-struct alignas(64) Node4q {
-    float origin[3];       // 12 B: the grid's corner (f32), at or below every child's lower planes
-    int8_t exp[3];         // 3 B: grid step 2^exp per axis
-    uint8_t pad0;
-    uint32_t q[6];         // 24 B: plane j of the 4 children, byte k = child k
-    int32_t pad1[2];       // 8 B
-    int32_t child[4];      // 16 B: as Node4
-};
-static_assert(sizeof(Node4q) == 64, "Node4q must be half a 128-B line");
-
 // Triangle vertices in traversal-BVH leaf order, 80 B for 16-B aligned loads.  `rank` is the
 // triangle's scene-wide position in the REFERENCE tree's in-order leaf sequence (tri_base + leaf
 // position of the median-split build): equal-distance hits go to the higher rank, as
@@ -126,7 +108,6 @@ struct Bvh {
 struct DeviceScene {
     const Node* nodes;     // binary tree (trace / shadow rays)
     const Node4* nodes4;   // 4-wide traversal tree (render kernel)
-    const Node4q* nodes4q; // the same quantised to 64 B per node (large trees), or nullptr
     const TriVerts* tris;
     const TriNormals* normals;
     const Material* materials;
@@ -246,7 +227,6 @@ struct LaunchChoice {
     int mats;         // material kinds present (bit 0 Lambertian, 1 reflective, 2 Phong / dielectric)
     bool coop;        // the cooperative-tail instantiation (RenderArgs::coop set; never with the above)
     bool big;         // 64-bit node / triangle load offsets (vr_host.cpp needs_big_offsets)
-    bool qnode;       // the node step reads DeviceScene::nodes4q (vr_host.cpp use_quantized_nodes)
 };
 int launch_render(const RenderArgs& args, const LaunchChoice& choice, int grid_limit, void* stream,
                   void* mid_event = nullptr);
@@ -268,10 +248,7 @@ int device_build_bvh(const double* verts, const double* norms, uint32_t n, int32
 // device (root at nodes[0]); the triangles are permuted into its leaf order
 int device_build_sah(TriVerts* tris, TriNormals* normals, uint32_t n, int32_t node_base, int32_t tri_base,
                      Node* nodes, double* root_box, int* levels, void* stream);
-// vr_build.hip: the quantised copy of a device 4-wide tree (vr_qnode.h); *bad (device) counts nodes
-// whose boxes are not finite (then the quantised tree must not be used)
-int device_quantize_wide(const Node4* in, uint64_t n, Node4q* out, unsigned int* bad, void* stream);
-// vr_build.hip: Node4 records from a device-built binary tree and a host-made descriptor
+// vr_build.hip: Node4 / Node4x records from a device-built binary tree and a host-made descriptor
 int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
 const char* device_error_string(int code);

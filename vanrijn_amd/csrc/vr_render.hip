@@ -116,9 +116,6 @@ constexpr int kPrioA = 0, kPrioNode = 1, kPrioLeaf = 1;
 #ifndef VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
 #define VR_WATCHDOG 0
 #endif
-#ifndef VR_COOP_SORT  // the cooperative tail pushes its frontier near-first (coop_step)
-#define VR_COOP_SORT 1
-#endif
 constexpr int kPend = 8;  // FIFO entries per lane of a wave, on average
 constexpr int kWaveList = 64 * kPend;
 static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
@@ -138,7 +135,6 @@ __device__ __forceinline__ KArgs kargs() {
 }
 #define VR_NODES4 (kargs()->scene.nodes4)
 #define VR_TRIS (kargs()->scene.tris)
-#define VR_NODES4Q (kargs()->scene.nodes4q)
 
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
@@ -150,10 +146,8 @@ enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3,
 // BIG: 64-bit byte offsets for the node and triangle loads -- scenes whose triangle array reaches 4 GB
 // (53.7 M triangles) or whose 4-wide tree has 2^25 nodes (vr_host.cpp needs_big_offsets); every other
 // scene's kernels address both arrays with 32-bit offsets from the scalar base (the loads' saddr form)
-// QNODE: the node step reads the 64-B quantised nodes (Node4q, vr_qnode.h) instead of the 128-B
-// Node4 -- large trees, whose traversal is bound by L2 misses (C5); never with COOP
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          bool COOP = false, bool BIG = false, bool QNODE = false>
+          bool COOP = false, bool BIG = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
@@ -256,10 +250,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     auto node_at = [&](int n) -> const Node4& {
         if (BIG) return VR_NODES4[(uint32_t)n];
         return *(const Node4*)((const char*)VR_NODES4 + ((uint32_t)n << 7));
-    };
-    auto qnode_at = [&](int n) -> const Node4q* {
-        if (BIG) return VR_NODES4Q + (uint32_t)n;
-        return (const Node4q*)((const char*)VR_NODES4Q + ((uint32_t)n << 6));
     };
     auto takes_hit = [&](double d, uint32_t rk) {
         const bool closer = !best.kind | (d < best.d);
@@ -739,7 +729,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         const bool work = t > 0 && VR_ROOM;  // uniform per half
         uint32_t im = 0;                     // hit interior children
         int c[4] = {0, 0, 0, 0};
-        float fk[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // their f32 entry distances
         int pos = o_sp;
         if (work) {
             VR_MARK("coop_step");
@@ -773,7 +762,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     const bool lv = c[k] != kEmptyChild;
                     if (COUNT && lv) cnt.box_tests++;
                     const bool pass = lv && maybe && !(f > cf || g < cb);
-                    fk[k] = f;
                     xm |= (pass && !sure) ? 1u << k : 0u;
                     im |= (pass && c[k] >= 0) ? 1u << k : 0u;
                     lmask |= (pass && c[k] < 0) ? 1u << k : 0u;
@@ -781,69 +769,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
             }
         }
-#if VR_COOP_SORT
-        // interior hits onto the owner's stack near-first: the owner pops the top, so
-        // the walk follows the nearest child found in the step as the per-lane walk does.  Each
-        // worker orders its hit children by packed key (the node step's: the entry distance's bits
-        // over the child index, A.sort_mask); the workers are ordered, across the owner's lanes, by
-        // their nearest key, farthest first (a bitonic network of lane shuffles on one 64-bit key per
-        // lane: nearest key << 32 | worker); every worker writes its children farthest-first from
-        // its place in that order.  Top of stack: the step's nearest child; below it the rest of its
-        // worker's, then the next-nearest worker's.  Only the visiting order changes (DESIGN.md
-        // section 5: the closest hit and its tie rule do not depend on it).
-        {
-            const uint32_t smask = A.sort_mask;
-            uint32_t key[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool h = (im >> k) & 1u;
-                key[k] = h ? (((uint32_t)max(__float_as_int(fk[k]), 0) & ~smask) | (uint32_t)c[k]) : 0xffffffffu;
-            }
-            auto cas = [&](int i, int j) {
-                const uint32_t ki = key[i], kj = key[j];
-                key[i] = ki < kj ? ki : kj;
-                key[j] = ki < kj ? kj : ki;
-            };
-            cas(0, 1);
-            cas(2, 3);
-            cas(0, 2);
-            cas(1, 3);
-            cas(1, 2);  // ascending: key[0] the worker's nearest
-            const int nh = (int)__popc(im);
-            // one record per lane of the group, sorted DESCENDING by (nearest key, worker rank): the
-            // worker with no hit (key 0xffffffff) sorts first and pushes nothing
-            uint64_t rec = ((uint64_t)key[0] << 32) | (uint32_t)r;
-            for (int kk = 2; kk <= gsize; kk <<= 1) {
-                for (int j = kk >> 1; j > 0; j >>= 1) {
-                    const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(rec >> 32), j) << 32) |
-                                       (uint32_t)__shfl_xor((int)(uint32_t)rec, j);
-                    const bool lower = (r & j) == 0, desc = (r & kk) == 0;
-                    // descending blocks keep the larger record in the lower lane
-                    const bool keep_max = lower == desc;
-                    rec = keep_max ? (rec > o ? rec : o) : (rec < o ? rec : o);
-                }
-            }
-            // position r of the order holds worker w = rec's low half; its pushes start after the
-            // pushes of positions < r: an exclusive prefix sum of the workers' hit counts in order
-            const int w = (int)(uint32_t)rec;
-            int cntw = __shfl(nh, gbase + w);
-            int incl = cntw;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                if (d >= gsize) break;
-                const int v = __shfl_up(incl, (unsigned)d, gsize);
-                if (r >= d) incl += v;
-            }
-            const int excl = incl - cntw;
-            // hand each worker its start: lane gbase + r sends `excl` to lane gbase + w
-            const int start = __builtin_amdgcn_ds_permute((gbase + w) << 2, excl);
-            // farthest first: key[nh - 1] lowest, key[0] on top
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < nh) st_node[coop_vaddr(owner, om, pos + start + (nh - 1 - k))] = key[k] & smask;
-            pos += __shfl(incl, gbase + gsize - 1);  // all the group's pushes
-        }
-#else
         // interior hits onto the owner's stack, in (child slot, worker) order
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -852,7 +777,6 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             if (ih) st_node[coop_vaddr(owner, om, pos + (int)lanes_below(m))] = (uint32_t)c[k];
             pos += (int)__popcll(m);
         }
-#endif
         // each owner takes its next node, the top of its stack: its workers' pos and work flag
         // (uniform over its half) by permute from the half's first lane
         const int lead = (two && (int)lane == ob) ? 32 : 0;
@@ -1098,6 +1022,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 VR_MARK("node_step");
                 // 32-bit byte offset from the scalar base (node < 2^25 unless BIG): the load's saddr form,
                 // no 64-bit address arithmetic per step
+                const Node4& nd = node_at(node);
                 if (COUNT) cnt.node_visits++;
                 int c[4];
                 float f[4];
@@ -1108,35 +1033,17 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 // test runs in the leaf round, beside the triangle test (the f32 bounds tlo / thi
                 // enclose the exact interval either way, so the f32 cull stays conservative)
                 uint32_t hm = 0, xm = 0;
-                auto child_flags = [&](int k, float g, bool maybe, bool sure) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    c[k] = nd.child[k];
+                    float g;
+                    bool maybe, sure;
+                    slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
                     const bool live = c[k] != kEmptyChild;
                     if (COUNT && live) cnt.box_tests++;
                     const bool pass = live && maybe && !(f[k] > cull_far || g < cull_behind);
                     hm |= pass ? 1u << k : 0u;
                     xm |= (pass && !sure) ? 1u << k : 0u;
-                };
-                if constexpr (QNODE) {
-                    // the quantised node: one 64-B record, the grid's slab constants once per node
-                    const Node4q nq = load_node4q(qnode_at(node));
-                    const QFrame qf = qframe(nq, pre32);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        c[k] = nq.child[k];
-                        float g;
-                        bool maybe, sure;
-                        slab32q_flags(nq, k, qf, pre32, f[k], g, maybe, sure);
-                        child_flags(k, g, maybe, sure);
-                    }
-                } else {
-                    const Node4& nd = node_at(node);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        c[k] = nd.child[k];
-                        float g;
-                        bool maybe, sure;
-                        slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
-                        child_flags(k, g, maybe, sure);
-                    }
                 }
                 // leaf children: their triangles go to the wave FIFO, appended after the step by all
                 // lanes at once
@@ -1601,22 +1508,6 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
         }
         return launch_reduce(a, s, mid);
     }
-    if (c.qnode) {
-        // quantised nodes (large trees): the Lambertian-only DARK0 kernels (C5) and the general
-        // ones, in the stack classes 32 and 48 only (launch_render)
-        if constexpr (STACK < 32) return hipErrorInvalidValue;
-        else if (a.scene.integrator == 1) return hipErrorInvalidValue;  // (never chosen: vr_host.cpp)
-        else if (c.dark0 && c.mats == 1) {
-            if (recording) VR_K(STACK, false, true, true, 1, 3, false, false, false, true);
-            else if (counting) VR_K(STACK, true, false, true, 1, 3, false, false, false, true);
-            else VR_K(STACK, false, false, true, 1, 3, false, false, false, true);
-        } else {
-            if (recording) VR_K(STACK, false, true, false, 3, 3, false, false, false, true);
-            else if (counting) VR_K(STACK, true, false, false, 3, 3, false, false, false, true);
-            else VR_K(STACK, false, false, false, 3, 3, false, false, false, true);
-        }
-        return launch_reduce(a, s, mid);
-    }
     if (a.scene.integrator == 1) {  // WhittedIntegrator: the general-material kernel
         if (recording) VR_K(STACK, false, true, true, 3, 3, true);
         else if (counting) VR_K(STACK, true, false, true, 3, 3, true);
@@ -1685,7 +1576,6 @@ int launch_render(const RenderArgs& a, const LaunchChoice& c, int grid_limit, vo
     // the 64-bit-offset kernels exist in the deepest stack class only (a scene that needs them is
     // far larger than any whose tree fits the smaller classes; more LDS is only fewer waves)
     if (c.big && c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);
-    else if (c.qnode && c.stack_depth <= 32) e = launch_render_t<32>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 24) e = launch_render_t<24>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 32) e = launch_render_t<32>(a, c, grid_limit, s, mid);
     else if (c.stack_depth <= 48) e = launch_render_t<48>(a, c, grid_limit, s, mid);

@@ -305,12 +305,11 @@ class Scene:
         return self._spec
 
     def device_scene(self, device=0, host_only=False, device_bvh=False, reference_bvh=False, device_sah=False,
-                     wide_offsets=False, quantized_nodes=None):
-        key = (device, host_only, device_bvh, reference_bvh, device_sah, wide_offsets, quantized_nodes)
+                     wide_offsets=False):
+        key = (device, host_only, device_bvh, reference_bvh, device_sah, wide_offsets)
         if key not in self._device_scenes:
             self._device_scenes[key] = DeviceScene(self.spec(), device, host_only, device_bvh, reference_bvh,
-                                                   device_sah, wide_offsets=wide_offsets,
-                                                   quantized_nodes=quantized_nodes)
+                                                   device_sah, wide_offsets=wide_offsets)
         return self._device_scenes[key]
 
 
@@ -318,15 +317,13 @@ class DeviceScene:
     """Owner of a `vr_scene*` (flattened BVH resident in one GPU's HBM)."""
 
     def __init__(self, spec: SceneSpec, device=0, host_only=False, device_bvh=False, reference_bvh=False,
-                 device_sah=False, greedy_collapse=False, wide_offsets=False, quantized_nodes=None):
+                 device_sah=False, greedy_collapse=False, wide_offsets=False):
         """device_bvh: build the BVHs on the GPU (VR_SCENE_DEVICE_BVH: the reference's tree);
         reference_bvh: traverse the reference's median-split tree instead of the SAH tree;
         device_sah: build the SAH traversal tree on the GPU too (VR_SCENE_DEVICE_SAH);
         greedy_collapse: the greedy 4-wide collapse instead of the SAH-optimal one (inspection);
         wide_offsets: render with the 64-bit-offset kernels that scenes past 53.7 M triangles or 2^25
-        wide nodes take automatically (VR_SCENE_WIDE_OFFSETS; identical renders);
-        quantized_nodes: True / False force the 64-B quantised 4-wide nodes on / off, None picks by
-        tree size (VR_SCENE_QUANTIZED_NODES / VR_SCENE_FULL_NODES; identical renders)."""
+        wide nodes take automatically (VR_SCENE_WIDE_OFFSETS; identical renders)."""
         L = N.lib()
         self.spec = spec
         keep = []  # keep ctypes buffers alive during vr_scene_create
@@ -373,9 +370,7 @@ class DeviceScene:
         h = C.c_void_p()
         flags = ((N.SCENE_HOST_ONLY if host_only else 0) | (N.SCENE_DEVICE_BVH if device_bvh else 0) |
                  (N.SCENE_REFERENCE_BVH if reference_bvh else 0) | (N.SCENE_DEVICE_SAH if device_sah else 0) |
-                 (N.SCENE_GREEDY_COLLAPSE if greedy_collapse else 0) | (N.SCENE_WIDE_OFFSETS if wide_offsets else 0) |
-                 (N.SCENE_QUANTIZED_NODES if quantized_nodes is True else 0) |
-                 (N.SCENE_FULL_NODES if quantized_nodes is False else 0))
+                 (N.SCENE_GREEDY_COLLAPSE if greedy_collapse else 0) | (N.SCENE_WIDE_OFFSETS if wide_offsets else 0))
         N.check(L.vr_scene_create(C.byref(desc), device, flags, C.byref(h)))
         self.handle = h
         self.device = device
@@ -405,7 +400,6 @@ class DeviceScene:
         N.check(N.lib().vr_scene_get_info(self.handle, C.byref(i)))
         d = {n: getattr(i, n) for n, _ in i._fields_}
         d["nan_free"] = bool(d["flags"] & N.SCENE_INFO_NAN_FREE)
-        d["quantized_nodes"] = bool(d["flags"] & N.SCENE_INFO_QUANTIZED_NODES)
         return d
 
     def set_fault_object(self, obj):
@@ -413,12 +407,12 @@ class DeviceScene:
         shading basis (VR_ERROR_SINGULAR_BASIS); -1 turns it off."""
         N.check(N.lib().vr_debug_set_fault_object(self.handle, obj))
 
-    def set_launch_flags(self, no_cull=False, no_dist_cull=False, no_coop=False, full_nodes=False):
+    def set_launch_flags(self, no_cull=False, no_dist_cull=False, no_coop=False):
         """Test hook (vr_debug_set_launch_flags): every later render of this scene -- per-sample
         records and host buffers included -- skips the frustum culling, the BVH distance culling or
         the cooperative tail (each leaves the records bit-identical)."""
         flags = ((N.LAUNCH_NO_CULL if no_cull else 0) | (N.LAUNCH_NO_DIST_CULL if no_dist_cull else 0) |
-                 (N.LAUNCH_NO_COOP if no_coop else 0) | (N.LAUNCH_FULL_NODES if full_nodes else 0))
+                 (N.LAUNCH_NO_COOP if no_coop else 0))
         N.check(N.lib().vr_debug_set_launch_flags(self.handle, flags))
 
     NODE_DTYPE = np.dtype([("box", "<f8", (2, 6)), ("child", "<i4", (2,)), ("pad", "<i4", (6,))])
