@@ -229,7 +229,7 @@ typedef struct vr_accumulation_buffer {
 } vr_accumulation_buffer;
 
 /* Sampling parameters.  Each (pixel, sample) draws its random numbers from the counter-based
- * stream (seed, row*width+column, first_sample + s) ("vr-splitmix v1"), so results do
+ * stream (seed, row*width+column, first_sample + s) ("vr-hash32 v2"), so results do
  * not depend on tiling, launch split or device count. */
 typedef struct vr_render_params {
     vr_tile tile;

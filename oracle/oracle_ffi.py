@@ -57,6 +57,7 @@ def lib():
         d, p, u64, i64, i32, u32 = C.c_double, C.c_void_p, C.c_uint64, C.c_int64, C.c_int32, C.c_uint32
         sig = {
             "orc_mix64": (u64, [u64]),
+            "orc_hash32": (C.c_uint32, [C.c_uint32]),
             "orc_stream_base": (u64, [u64, u64, u64]),
             "orc_stream_draw": (u64, [u64, u64]),
             "orc_u64_to_standard": (d, [u64]),

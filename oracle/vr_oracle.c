@@ -22,24 +22,42 @@
 #include <string.h>
 
 /* ======================================================================================== */
-/* Random stream "vr-splitmix v1" (replaces rand 0.7 ThreadRng)          */
+/* Random stream "vr-hash32 v2" (replaces rand 0.7 ThreadRng)  */
 /* ======================================================================================== */
-#define ORC_GOLDEN 0x9E3779B97F4A7C15ULL
 #define ORC_SEED_SALT 0x76616E52696A6E31ULL /* "vanRijn1" */
+#define ORC_WEYL32 0x9E3779B9u            /* the draw counter's step */
+#define ORC_LO_OFFSET 0x6A09E667u         /* the low word hashes the counter plus this */
 
-uint64_t orc_mix64(uint64_t z) {
+uint64_t orc_mix64(uint64_t z) { /* splitmix64's finaliser */
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
 
-uint64_t orc_stream_base(uint64_t seed, uint64_t pixel_index, uint64_t sample_index) {
-    uint64_t k = orc_mix64(seed ^ ORC_SEED_SALT);
-    k = orc_mix64(k + pixel_index);
-    return orc_mix64(k + sample_index);
+/* Wellons' "lowbias32" 32-bit integer hash (two multiplies; a bijection) */
+uint32_t orc_hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
 }
 
-uint64_t orc_stream_draw(uint64_t base, uint64_t k) { return orc_mix64(base + (k + 1) * ORC_GOLDEN); }
+/* the per-(pixel, sample) stream base: one mix of the key and the (pixel, sample) pair as one 64-bit
+ * word (injective for pixel, sample < 2^32), keyed by the seed */
+uint64_t orc_stream_base(uint64_t seed, uint64_t pixel_index, uint64_t sample_index) {
+    const uint64_t key = orc_mix64(seed ^ ORC_SEED_SALT);
+    return orc_mix64(key ^ ((pixel_index << 32) + sample_index));
+}
+
+/* draw k (0-based): a 32-bit Weyl counter from the base's low word, xored with its high word, hashed
+ * twice (high word: the counter, low word: the counter plus a constant) */
+uint64_t orc_stream_draw(uint64_t base, uint64_t k) {
+    const uint32_t x = (uint32_t)base + (uint32_t)(k + 1) * ORC_WEYL32;
+    const uint32_t v = x ^ (uint32_t)(base >> 32);
+    return ((uint64_t)orc_hash32(v) << 32) | orc_hash32(v + ORC_LO_OFFSET);
+}
 
 /* rand 0.7 `Standard` for f64: 53 high bits times 2^-53 (camera.rs:49, photon.rs:21) */
 double orc_u64_to_standard(uint64_t u) { return (double)(u >> 11) * 0x1.0p-53; }

@@ -21,7 +21,7 @@
  *     reflection_from_linear_rgb, CMF values, whole images.  Restated line by line instead.
  *   - The reference draws from rand 0.7's ThreadRng (ChaCha, reseeded from OS entropy, cannot be
  *     seeded: SURVEY.md F4).  The oracle and the product both draw from the counter-based
- *     "vr-splitmix v1" stream defined below; the u64 -> f64 maps follow rand 0.7's Standard and
+ *     "vr-hash32 v2" stream defined below; the u64 -> f64 maps follow rand 0.7's Standard and
  *     Open01 (parity of those maps: unpinned, no reference test covers them).
  *
  * Build: oracle/Makefile (gcc, -O2 -ffp-contract=off: Rust never contracts a*b+c into an FMA).
@@ -38,6 +38,7 @@ extern "C" {
 
 /* ---- random stream (shared definition with the product, restated independently there) ---- */
 uint64_t orc_mix64(uint64_t z);
+uint32_t orc_hash32(uint32_t x);
 uint64_t orc_stream_base(uint64_t seed, uint64_t pixel_index, uint64_t sample_index);
 uint64_t orc_stream_draw(uint64_t base, uint64_t k);
 double orc_u64_to_standard(uint64_t u); /* rand 0.7 Standard f64: [0,1) */

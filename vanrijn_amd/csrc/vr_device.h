@@ -80,21 +80,40 @@ __device__ __forceinline__ double sel(V3 v, int k) { return k == 0 ? v.x : (k ==
 __device__ __forceinline__ V3 ldv(const double* p) { return mk(p[0], p[1], p[2]); }
 
 // ----------------------------------------------------------------------------------------------
-// Random stream "vr-splitmix v1" + rand 0.7 maps (same definition as oracle/vr_oracle.c)
+// Random stream "vr-hash32 v2" + rand 0.7 maps (same definition as oracle/vr_oracle.c; DESIGN.md
+// section 3).  Per (pixel, sample) one 64-bit base, mix64(key ^ (pixel << 32 | sample)), then draw k
+// hashes a 32-bit Weyl counter (base's low word + k * 0x9E3779B9) xored with base's high word twice
+// with Wellons' lowbias32 -- 12 VALU (4 of them v_mul_lo_u32) per 64-bit draw, against 17 (a 64-bit
+// xorshift-multiply finaliser: 3 v_lshrrev_b64, 2 v_mad_u64_u32, 4 v_mul_lo_u32) for splitmix64's
+// finaliser per draw and two per base in round 4's "vr-splitmix v1" (draw mixing measured at 7.6 %
+// of the C3 launch's VALU instructions, profiles/r05/rng).
 // ----------------------------------------------------------------------------------------------
-constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kSeedSalt = 0x76616E52696A6E31ull;
+constexpr uint32_t kWeyl32 = 0x9E3779B9u;
+constexpr uint32_t kLoOffset = 0x6A09E667u;
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {  // lowbias32
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
 struct Rng {
-    uint64_t cur;  // base + k * kGolden after k draws: draw k + 1 adds kGolden (no 64-bit multiply)
-    __device__ __forceinline__ void reset(uint64_t base) { cur = base; }
+    uint32_t x, y;  // the draw counter (base's low word + k * kWeyl32 after k draws) and base's high word
+    __device__ __forceinline__ void reset(uint64_t base) {
+        x = (uint32_t)base;
+        y = (uint32_t)(base >> 32);
+    }
     __device__ __forceinline__ uint64_t next() {
-        cur += kGolden;
-        return mix64(cur);
+        x += kWeyl32;
+        const uint32_t v = x ^ y;
+        return ((uint64_t)hash32(v) << 32) | hash32(v + kLoOffset);
     }
     // rand 0.7 Standard f64 (camera.rs:49, photon.rs:21)
     __device__ __forceinline__ double standard() { return (double)(next() >> 11) * 0x1.0p-53; }
@@ -106,14 +125,9 @@ struct Rng {
     // the u32 is the draw's high half, so the bool is the draw's top bit
     __device__ __forceinline__ bool boolean() { return (int32_t)(uint32_t)(next() >> 32) < 0; }
 };
-__device__ __forceinline__ uint64_t stream_base(uint64_t seed, uint64_t pixel, uint64_t sample) {
-    uint64_t k = mix64(seed ^ kSeedSalt);
-    k = mix64(k + pixel);
-    return mix64(k + sample);
-}
-// the same, from seed_key = mix64(seed ^ kSeedSalt) (a per-launch constant, RenderArgs::seed_key)
+// the stream base from seed_key = mix64(seed ^ kSeedSalt) (a per-launch constant, RenderArgs::seed_key)
 __device__ __forceinline__ uint64_t stream_base_keyed(uint64_t seed_key, uint64_t pixel, uint64_t sample) {
-    return mix64(mix64(seed_key + pixel) + sample);
+    return mix64(seed_key ^ ((pixel << 32) + sample));
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -1002,7 +1002,7 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.width = p->width;
     a.height = p->height;
     a.seed = p->seed;
-    {  // vr-splitmix v1: the launch-constant first step of stream_base
+    {  // vr-hash32 v2: the launch-constant key of stream_base_keyed
         uint64_t z = p->seed ^ 0x76616E52696A6E31ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;

@@ -134,7 +134,7 @@ struct RenderArgs {
     uint64_t start_column, start_row, tile_width, tile_height;
     uint64_t width, height;
     uint64_t seed, first_sample;  // absolute index of this pass's sample 0
-    uint64_t seed_key;            // mix64(seed ^ salt): stream_base's first step, once per launch
+    uint64_t seed_key;            // mix64(seed ^ salt): the stream key, once per launch
     uint32_t spp;                 // samples in this pass
     uint32_t accumulate;
     uint32_t shade_threshold;     // lanes finished with traversal before the wave shades

@@ -419,13 +419,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         best.index = -1;
         best.rank = 0;
         best.object = 0x7fffffff;
+        VR_MARK("br_prims");
         for (int i = 0; i < S.prim_count; ++i) {
             const Prim& pr = S.prims[i];
             double dd;
             bool ok;
             if (pr.kind == 0) {
+                VR_MARK("br_plane");
                 ok = plane_distance(pr, pre, dd);
             } else {
+                VR_MARK("br_sphere");
                 // the f64 test is skipped only when, for every lane, the line clearly misses the
                 // sphere or the sphere lies behind the origin or beyond the lane's best distance
                 // (camera rays of a wave are coherent; so are many bounce rays)
@@ -443,6 +446,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 best.object = pr.object;
             }
         }
+        VR_MARK("br_bvhs");
         set_cull_far();
         if (pre.behind_ok()) {
             cull_behind = round_away_f32(-S.behind_margin - margin_of(pre32));
