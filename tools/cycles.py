@@ -52,4 +52,10 @@ if len(c) >= 33:
     out["node_step_iterations"] = steps
     out["node_step_iterations_perfectly_packed"] = packed
     out["node_step_lane_utilisation"] = round(st["node_visits"] / (64.0 * max(1, steps)), 4)
+if len(c) >= 36:
+    # wave-level f64 sphere tests (begin_ray): how many ran, and how many of their lanes the f32
+    # pre-test left (the rest of the active lanes only follow along)
+    out["sphere_tests"] = {"wave_executions": int(c[33]), "maybe_lanes": int(c[34]), "active_lanes": int(c[35]),
+                           "maybe_lanes_per_execution": round(float(c[34]) / max(1, int(c[33])), 2),
+                           "active_lanes_per_execution": round(float(c[35]) / max(1, int(c[33])), 2)}
 print(json.dumps(out))

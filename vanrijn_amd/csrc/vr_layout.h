@@ -150,6 +150,10 @@ struct RenderArgs {
     uint32_t coop;
     uint32_t coop_bounces;
     uint32_t sort_mask;           // node step's packed child keys: low bits = child index (2^k - 1 > every wide node index)
+    // work-item order: 0 sample-major (item = (sample round, block, pixel): the chip's waves in flight
+    // cover the whole tile), 1 block-major (item = (block, sample round, pixel): they cover a few
+    // blocks, so their camera rays -- and the first hits' tree paths -- are shared)
+    uint32_t item_order;
     int32_t fault_object;         // test hook: hits on this object take the singular-basis path (-1: none)
     uint32_t shade_min;           // defer shading until this many lanes have hits (0: never defer)
     uint32_t miss_min;            // defer finishing misses until this many lanes missed (0: never)
@@ -213,7 +217,9 @@ enum Counter : int {
                              // finish, refill, start_bvhs in traversal
     kCntStepHist = 24,       // 24..32: phase-B iterations by the number n of lanes taking a node
                              // step in them: n = 0, then 1-8, 9-16, .., 57-64 (diagnostic, VR_COUNTERS_PATH)
-    kCntCount = 33
+    kCntPrimTests = 33,      // 33..35 (diagnostic, VR_COUNTERS_PATH): wave-level f64 sphere tests run,
+                             // their lanes whose f32 pre-test may hit, their active lanes
+    kCntCount = 36
 };
 
 // Launch wrappers implemented in vr_render.hip (host-callable).
@@ -234,7 +240,8 @@ int launch_render(const RenderArgs& args, const LaunchChoice& choice, int grid_l
 // the camera-frustum test of every 8x8 block of a launch's tile into mask (RenderArgs::block_mask)
 int launch_block_cull(const RenderArgs& args, uint8_t* mask, void* stream);
 // the live (unculled) blocks of `mask` (n blocks) in order into live[], their number into *count
-int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32_t* count, void* stream);
+int launch_block_compact(const uint8_t* mask, uint32_t bw, uint32_t bh, bool morton, uint32_t* live, uint32_t* count,
+                         void* stream);
 int launch_tonemap(const double* src, int from_state, uint64_t npix, uint8_t* rgb, void* stream);
 // vr_image.hip: device records (RenderArgs::state's layout) <-> the host AccumulationBuffer's five arrays laid
 // out back to back (to_planar = 1: records -> planar, 0: planar -> records; colour is not read;

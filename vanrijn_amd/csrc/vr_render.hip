@@ -181,6 +181,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     Counts cnt = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t sec[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t step_hist[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // counting variant: lanes per node step
+    uint32_t prim_cnt[3] = {0, 0, 0};  // counting variant: sphere tests, their maybe-lanes, active lanes
 #ifdef VR_MARKS  // ISA section markers for tools/isa_sections.py (analysis builds only)
 #define VR_MARK(name) asm volatile(";@mark " name)
 #else
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     const uint64_t per_chunk = (uint64_t)nlive * 64;
     const uint64_t items = render_items(A, per_chunk);
     const uint64_t rounds = chunk_rounds(A);
+    const double rcp_R = A.item_order ? 1.0 / (double)(rounds + tail_of(A)) : 0.0;  // block-major decode
     const uint32_t bulk = A.spp - tail_of(A);
     const uint64_t npix = A.tile_width * A.tile_height;
     uint32_t px = 0, py = 0, s_end = 0;
@@ -432,7 +434,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 // the f64 test is skipped only when, for every lane, the line clearly misses the
                 // sphere or the sphere lies behind the origin or beyond the lane's best distance
                 // (camera rays of a wave are coherent; so are many bounce rays)
-                if (sphere_maybe32_lanes(pr, pre) == 0) continue;
+                const uint64_t maybe_lanes = sphere_maybe32_lanes(pr, pre);
+                if (maybe_lanes == 0) continue;
+                if (COUNT) {
+                    const int act = __popcll(exec_mask());
+                    if (first_active_lane()) {
+                        prim_cnt[0]++;
+                        prim_cnt[1] += __popcll(maybe_lanes);
+                        prim_cnt[2] += act;
+                    }
+                }
                 {
                     const double a1 = sphere_a(pre.d);
                     dd = sphere_distance(pr, pre, a1, 1.0 / (2.0 * a1));
@@ -922,11 +933,25 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         // g = (chunk_i * blocks + blk) * 64 + l; g >> 6 < 2^32 (the host caps
                         // a launch's items), quotients by f64 reciprocal, corrected by one
                         const uint32_t gb = (uint32_t)(g >> 6), l = (uint32_t)(g & 63);
-                        const uint32_t nblk = (uint32_t)(per_chunk >> 6);
-                        uint32_t chunk_i = (uint32_t)((double)gb * rcp_live);
-                        int32_t rem = (int32_t)(gb - chunk_i * nblk);
-                        if (rem < 0) { --chunk_i; rem += (int32_t)nblk; }
-                        if (rem >= (int32_t)nblk) { ++chunk_i; rem -= (int32_t)nblk; }
+                        uint32_t chunk_i;
+                        int32_t rem;
+                        if (A.item_order) {
+                            // block-major: g = (blk * R + chunk_i) * 64 + l, R = the items per pixel
+                            // -- the waves in flight work on few blocks at a time (see RenderArgs)
+                            const uint32_t R = (uint32_t)(rounds + tail_of(A));
+                            uint32_t bi = (uint32_t)((double)gb * rcp_R);
+                            int32_t c = (int32_t)(gb - bi * R);
+                            if (c < 0) { --bi; c += (int32_t)R; }
+                            if (c >= (int32_t)R) { ++bi; c -= (int32_t)R; }
+                            rem = (int32_t)bi;
+                            chunk_i = (uint32_t)c;
+                        } else {
+                            const uint32_t nblk = (uint32_t)(per_chunk >> 6);
+                            chunk_i = (uint32_t)((double)gb * rcp_live);
+                            rem = (int32_t)(gb - chunk_i * nblk);
+                            if (rem < 0) { --chunk_i; rem += (int32_t)nblk; }
+                            if (rem >= (int32_t)nblk) { ++chunk_i; rem -= (int32_t)nblk; }
+                        }
                         const uint32_t blk = A.live_blocks ? A.live_blocks[rem] : (uint32_t)rem;
                         uint32_t by = (uint32_t)((double)blk * A.rcp_bw);
                         int32_t bx = (int32_t)(blk - by * bw);
@@ -1169,6 +1194,8 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         VR_STAMP(5);
         if (first_active_lane())
             for (int i = 0; i < 6; ++i) atomicAdd(&A.counters[kCntCycles + i], (unsigned long long)cyc[i]);
+        for (int i = 0; i < 3; ++i)
+            if (prim_cnt[i]) atomicAdd(&A.counters[kCntPrimTests + i], (unsigned long long)prim_cnt[i]);
         for (int i = 0; i < 9; ++i) {  // each lane counted the executions it led
             if (sec[i]) atomicAdd(&A.counters[kCntSections + i], (unsigned long long)sec[i]);
             if (step_hist[i]) atomicAdd(&A.counters[kCntStepHist + i], (unsigned long long)step_hist[i]);
@@ -1282,15 +1309,36 @@ __global__ __launch_bounds__(256) void block_cull_kernel(RenderArgs A, const Pri
     mask[b] = clear ? 1 : 0;
 }
 
-// The live blocks of a cull mask in block order (one workgroup: each thread counts a contiguous
-// run of blocks, an LDS scan gives the runs' offsets, then each thread writes its run's live ones).
-__global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask, uint32_t n, uint32_t* live,
-                                                              uint32_t* count) {
+// The live blocks of a cull mask (one workgroup: each thread counts a contiguous run of the index
+// space, an LDS scan gives the runs' offsets, then each thread writes its run's live blocks).  The
+// index space is the blocks in row-major order, or (morton) the Z-order curve over the tile's
+// blocks padded to a power-of-two square: with block-major work items (RenderArgs::item_order) the
+// waves in flight then cover a compact square of the image instead of a strip.
+__device__ __forceinline__ uint32_t vr_compact1by1(uint32_t x) {
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+__global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask, uint32_t bw, uint32_t bh,
+                                                              uint32_t side, uint32_t* live, uint32_t* count) {
     __shared__ uint32_t part[1024];
+    const uint32_t n = side ? side * side : bw * bh;  // the index space
+    auto block_of = [&](uint32_t i) -> int64_t {    // the live block at index i, or -1
+        uint32_t b = i;
+        if (side) {
+            const uint32_t x = vr_compact1by1(i), y = vr_compact1by1(i >> 1);
+            if (x >= bw || y >= bh) return -1;
+            b = y * bw + x;
+        }
+        return mask[b] == 0 ? (int64_t)b : -1;
+    };
     const uint32_t tid = threadIdx.x, per = (n + 1023) / 1024;
     const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
     uint32_t c = 0;
-    for (uint32_t i = lo; i < hi; ++i) c += mask[i] == 0;
+    for (uint32_t i = lo; i < hi; ++i) c += block_of(i) >= 0;
     part[tid] = c;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
@@ -1300,8 +1348,10 @@ __global__ __launch_bounds__(1024) void block_compact_kernel(const uint8_t* mask
         __syncthreads();
     }
     uint32_t off = part[tid] - c;
-    for (uint32_t i = lo; i < hi; ++i)
-        if (mask[i] == 0) live[off++] = i;
+    for (uint32_t i = lo; i < hi; ++i) {
+        const int64_t b = block_of(i);
+        if (b >= 0) live[off++] = (uint32_t)b;
+    }
     if (tid == 1023) *count = part[1023];
 }
 
@@ -1567,8 +1617,17 @@ int launch_block_cull(const RenderArgs& a, uint8_t* mask, void* stream) {
     return (int)hipGetLastError();
 }
 
-int launch_block_compact(const uint8_t* mask, uint32_t n, uint32_t* live, uint32_t* count, void* stream) {
-    hipLaunchKernelGGL(dev::block_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, n, live, count);
+int launch_block_compact(const uint8_t* mask, uint32_t bw, uint32_t bh, bool morton, uint32_t* live, uint32_t* count,
+                         void* stream) {
+    // Z-order only for near-square block grids (the padded square at most 4x the blocks)
+    uint32_t side = 0;
+    if (morton) {
+        side = 1;
+        while (side < bw || side < bh) side <<= 1;
+        if ((uint64_t)side * side > 4ull * bw * bh || side > 32768) side = 0;
+    }
+    hipLaunchKernelGGL(dev::block_compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, bw, bh, side, live,
+                       count);
     return (int)hipGetLastError();
 }
 
