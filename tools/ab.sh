@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B library builds on the GPU box: alternating processes, main 256 spp + bench 32 spp per library.
 #   ROUNDS=3 bash tools/ab.sh path/to/libA.so path/to/libB.so [more libraries ...]
+# SCENES: "scene:spp[:size] ..." (default "main:256 bench:32", size 1024)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -11,7 +12,8 @@ SCENES=${SCENES:-"main:256 bench:32"}
 for r in $(seq 1 "$R"); do
   for L in "$@"; do
     for sc in $SCENES; do
-      VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene ${sc%%:*} --spp ${sc##*:} --reps 2 --variants 0 \
+      IFS=: read -r SC SPP SZ <<< "$sc"
+      VR_LIBRARY="$L" timeout -k 10 300 python tools/variants.py --scene $SC --spp $SPP --size ${SZ:-1024} --reps 2 --variants 0 \
           --thresholds 52 2>> gpurun_out/variants.err | sed "s|^|$(basename "$L") |" >> gpurun_out/ab_libs.jsonl
       rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; exit $rc; }
     done
