@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 8
+#define VR_ABI_VERSION 9
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -296,6 +296,9 @@ typedef struct vr_launch_stats {
 /* no cooperative tail (small launches of scenes with a reflective material otherwise spread a
  * wave's last one or two paths over its lanes): the same records bit for bit (ABI 8) */
 #define VR_LAUNCH_NO_COOP 32u
+/* cooperative tail without its whole-walk form (the one or two live paths' walks run in coop_step's
+ * per-step form only): the same records bit for bit; for tests and A/B measurements (ABI 9) */
+#define VR_LAUNCH_NO_LONE_WALK 64u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);
@@ -392,7 +395,7 @@ int vr_scene_set_staging_limit(vr_scene* scene, uint64_t bytes);
  * calls on the same scene: set it before rendering (tests/test_gpu_concurrency.py).  ABI 5. */
 int vr_debug_set_fault_object(vr_scene* scene, int32_t object);
 
-/* Test hook: launch flags (VR_LAUNCH_NO_CULL / _NO_DIST_CULL / _NO_COOP only) applied to every render
+/* Test hook: launch flags (VR_LAUNCH_NO_CULL / _NO_DIST_CULL / _NO_COOP / _NO_LONE_WALK only) applied to every render
  * call of the scene, including the host-buffer and per-sample record entry points that take no launch
  * flags of their own; 0 turns them off.  Set before rendering, like the fault object (ABI 8). */
 int vr_debug_set_launch_flags(vr_scene* scene, uint32_t flags);

@@ -42,7 +42,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 8
+    assert lib.vr_abi_version() == 9
     assert isinstance(lib.vr_last_error(), bytes)
 
 
@@ -65,7 +65,7 @@ def test_debug_launch_flags_validated():
     from vanrijn_amd import scenes
     ds = scenes.bench_scene(scenes.displaced_mesh(6, [], 1, 0, 0.0, (1, 1, 1), (0, 0, 0))).device_scene(
         0, host_only=True)
-    ds.set_launch_flags(no_cull=True, no_dist_cull=True, no_coop=True)
+    ds.set_launch_flags(no_cull=True, no_dist_cull=True, no_coop=True, no_lone_walk=True)
     ds.set_launch_flags()
     try:
         N.check(N.lib().vr_debug_set_launch_flags(ds.handle, N.LAUNCH_TIMED))

@@ -84,20 +84,23 @@ def test_build_meshes_without_distance_culling(kind, oracle):
 
 def test_cooperative_tail_is_bit_identical():
     """C1 (benches/simple_scene.rs: reflective bunny, 256^2 @16): the COOP instantiation runs (the
-    launch reports it) and its records equal the plain kernel's, fresh and accumulating."""
+    launch reports it) and its records equal the plain kernel's, fresh and accumulating -- with the
+    whole-walk form (lone_walk, one and two owners per wave) and in coop_step's per-step form only."""
     ds = scenes.bench_scene().device_scene(0)
     H = W = 256
     t = Tile(0, W, 0, H)
     stream = torch.cuda.current_stream().cuda_stream
     out = []
-    for coop in (True, False):
+    for coop, lone in ((True, True), (True, False), (False, True)):
         st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
-        s1 = render_tile_device(ds, t, H, W, 16, 0x5EED0001, 0, st.data_ptr(), stream, coop=coop)
-        s2 = render_tile_device(ds, t, H, W, 5, 0x5EED0001, 16, st.data_ptr(), stream, accumulate=True, coop=coop)
+        s1 = render_tile_device(ds, t, H, W, 16, 0x5EED0001, 0, st.data_ptr(), stream, coop=coop, lone_walk=lone)
+        s2 = render_tile_device(ds, t, H, W, 5, 0x5EED0001, 16, st.data_ptr(), stream, accumulate=True, coop=coop,
+                                lone_walk=lone)
         torch.cuda.synchronize()
         assert bool(s1["variant"] & N.VARIANT_COOP) == coop and bool(s2["variant"] & N.VARIANT_COOP) == coop
         out.append(st.cpu())
-    assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
+    for o in out[1:]:
+        assert torch.equal(out[0].view(torch.int64), o.view(torch.int64))
     assert np.isfinite(out[0].numpy()).all()
 
 

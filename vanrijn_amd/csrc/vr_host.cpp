@@ -1066,7 +1066,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         const uint64_t lsamples = a.tile_width * a.tile_height * (uint64_t)p->spp;
         a.coop = (lsamples <= VR_COOP_SAMPLES && (s->mats & 2) && s->dark0) ? 2u : 0u;
         if (const char* co = tuning_env("VR_COOP")) a.coop = (uint32_t)std::min(2, std::max(0, atoi(co)));
-        a.coop_bounces = VR_COOP_BOUNCES;  // ... once every live path of the wave has bounced this often
+        a.coop_bounces = VR_COOP_BOUNCES;
+        a.lone_walk = 1;  // ... once every live path of the wave has bounced this often
         if (const char* cb = tuning_env("VR_COOP_BOUNCES")) a.coop_bounces = (uint32_t)std::max(0, atoi(cb));
     }
     {
@@ -1209,8 +1210,13 @@ int ctx_acquire(vr_scene* s, CallCtx** out, const hipStream_t* want = nullptr) {
     // blocking sync: a host-buffer call waits on `done` asleep, not spinning a core (8 spinning
     // callers under a 16-CPU quota throttled the whole process for ~10 ms at a time)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming | hipEventBlockingSync);
+#ifdef VR_COOP_PROF  // analysis builds: per-wave records after word 24 (vr_render.hip)
+    if (e == hipSuccess) e = hipMalloc(&c->queue, 65536);
+    if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, 65536, c->stream);
+#else
     if (e == hipSuccess) e = hipMalloc(&c->queue, 256);
     if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, 256, c->stream);
+#endif
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         ctx_free_all(c);
@@ -1651,8 +1657,9 @@ int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
 
 int vr_debug_set_launch_flags(vr_scene* s, uint32_t flags) {
     if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
-    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP;
-    if (flags & ~allowed) return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP apply to every call");
+    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP | VR_LAUNCH_NO_LONE_WALK;
+    if (flags & ~allowed)
+        return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP / NO_LONE_WALK apply to every call");
     s->debug_launch_flags = flags;
     return VR_OK;
 }
@@ -1790,6 +1797,7 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
             a.scene.behind_margin = INFINITY;
         }
         if (launch_flags & VR_LAUNCH_NO_COOP) a.coop = 0;
+        if (launch_flags & VR_LAUNCH_NO_LONE_WALK) a.lone_walk = 0;
 #ifdef VR_STAGE_GUARD
         a.stage_tag = (uint32_t*)c->tags;
         if (++c->gen == 0) c->gen = 1;
@@ -1803,6 +1811,20 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         a.records = records;
         a.counters = counters;
         a.wg_times = done == 0 ? wg_times : nullptr;
+#ifdef VR_COOP_PROF  // analysis builds: the previous launch's tail-wave sums (vr_render.hip)
+        {
+            static unsigned long long h[16 + 6000];
+            VR_HIP(hipStreamSynchronize(st));
+            VR_HIP(hipMemcpy(h, c->queue + 8, sizeof h, hipMemcpyDeviceToHost));
+            if (h[7])
+                fprintf(stderr, "vrcoop A %llu coop %llu leaf %llu rest %llu iters %llu leafrounds %llu phaseA %llu waves %llu maxwall %llu sumwall %llu lone %llu\n",
+                        h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]);
+            for (unsigned long long i = 0; i < h[11] && i < 1000; ++i)
+                fprintf(stderr, "vrwave %llu %llu %llu %llu %llu %llu\n", h[16 + 6 * i], h[17 + 6 * i], h[18 + 6 * i],
+                        h[19 + 6 * i], h[20 + 6 * i], h[21 + 6 * i]);
+            VR_HIP(hipMemset(c->queue + 8, 0, sizeof h));
+        }
+#endif
         VR_HIP(hipMemsetAsync(c->queue, 0, sizeof(unsigned long long), st));
         hipEvent_t mid = nullptr;
         if (timing) {

@@ -149,6 +149,8 @@ struct RenderArgs {
     // wave's lanes once each has bounced `coop_bounces` times; coop = owners served (0: off)
     uint32_t coop;
     uint32_t coop_bounces;
+    // 1: the tail's walks with nothing pending run whole in lone_walk (0: coop_step only; test hook)
+    uint32_t lone_walk;
     uint32_t sort_mask;           // node step's packed child keys: low bits = child index (2^k - 1 > every wide node index)
     // work-item order: 0 sample-major (item = (sample round, block, pixel): the chip's waves in flight
     // cover the whole tile), 1 block-major (item = (block, sample round, pixel): they cover a few

@@ -81,6 +81,33 @@ __device__ inline uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// lane l's value, wave-uniform (v_readlane into SGPRs; l uniform)
+__device__ __forceinline__ int rl_i32(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rl_f32(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ double rl_f64(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// minimum / maximum of v over the wave's 64 lanes (all active), wave-uniform
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint64_t w = __shfl_xor(v, s);
+        v = w < v ? w : v;
+    }
+    return uniform64(v);
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint64_t w = __shfl_xor(v, s);
+        v = w > v ? w : v;
+    }
+    return uniform64(v);
+}
+
 __host__ __device__ inline uint32_t tail_of(const RenderArgs& a) {
     return a.tail_samples < a.spp ? a.tail_samples : a.spp;
 }
@@ -197,6 +224,21 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         tprev = t_;                                           \
     }
     uint32_t samples_done = 0;
+#ifdef VR_COOP_PROF  // analysis builds: where a cooperative-tail wave's time goes (printf at its end)
+    uint64_t cp_t[4] = {0, 0, 0, 0}, cp_prev = 0;  // phase A, coop steps, leaf rounds, rest of phase B
+    uint32_t cp_n[4] = {0, 0, 0, 0};               // phase B iterations, leaf rounds, phase A entries, lone walks
+    uint64_t cp_r0 = 0;                            // s_memrealtime (100 MHz) when the wave's tail began
+    const uint64_t cp_s = __builtin_amdgcn_s_memrealtime();
+    uint32_t cp_maxlive = 0;
+#define VR_CP(i)                                              \
+    if (coop_on) {                                            \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        cp_t[i] += t_ - cp_prev;                              \
+        cp_prev = t_;                                         \
+    }
+#else
+#define VR_CP(i)
+#endif
     if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
     // work items run over the live blocks only (frustum-culled blocks are not in the item space)
@@ -823,10 +865,195 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         }
         q_tail = __builtin_amdgcn_readfirstlane(q_tail);
     };
+    // The cooperative tail's walks with nothing pending (no stack entries, no queued leaves, an empty
+    // wave FIFO) for the one or two traversing paths `own` of a wave whose other lanes are done: the
+    // whole rest of each path's walk of its current BVH in one call.  With one owner every lane
+    // works for it; with two the lower half works for the lower owner and the upper half for the
+    // other, both walks at once.  An owner's frontier of nodes to visit is a LIFO over its half's
+    // columns of the wave's stack words; each iteration pops up to one entry per worker, tests the
+    // entries' children against the owner's ray, pushes the hit interior children and tests the hit
+    // leaves at once, one per worker per round.  The round's candidate (minimum distance, then the
+    // highest reference rank) is merged with takes_hit's rule, as in leaf_round, so each path gets
+    // what its per-lane walk finds: only the visiting order differs.  Against coop_step it saves the
+    // per-step owner-state permutes and stack remapping and the separate leaf rounds through the FIFO
+    // (C1: the trapped mirror paths' last bounces).  Called with the whole wave active.
+    auto lone_walk = [&](const uint64_t own) {
+        const int oa = (int)__builtin_ctzll(own), ob = (int)(63 - __builtin_clzll(own));
+        const bool two = oa != ob;  // wave-uniform
+        const bool upper = two && lane >= 32;
+        const int hb = upper ? 32 : 0, hshift = two ? 5 : 6, hs = 1 << hshift;
+        const int r = (int)lane - hb;  // worker rank
+        const uint64_t gmask = two ? (upper ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
+        // this half's owner's ray, cull bounds and closest hit, by cross-lane permute (per-lane copies:
+        // uniform copies of both owners' values would need ~80 SGPRs, spilled)
+        const int ow = upper ? ob : oa;
+        auto p64 = [&](double v) { return __shfl(v, ow); };
+        auto p32 = [&](float v) { return __shfl(v, ow); };
+        auto pi = [&](int v) { return __shfl(v, ow); };
+        RayPre op;
+        op.o = mk(p64(pre.o.x), p64(pre.o.y), p64(pre.o.z));
+        op.d = mk(p64(pre.d.x), p64(pre.d.y), p64(pre.d.z));
+        op.sx = p64(pre.sx);
+        op.sy = p64(pre.sy);
+        op.pdz = p64(pre.pdz);
+        op.flags = pi(pre.flags);
+        Ray32 ry;
+        ry.ox = p32(pre32.ox); ry.oy = p32(pre32.oy); ry.oz = p32(pre32.oz);
+        ry.ix = p32(pre32.ix); ry.iy = p32(pre32.iy); ry.iz = p32(pre32.iz);
+        ry.nx = p32(pre32.nx); ry.ny = p32(pre32.ny); ry.nz = p32(pre32.nz);
+        ry.e2 = p32(pre32.e2);
+        float cf = p32(cull_far);
+        const float cb = p32(cull_behind);
+        const int cobj = pi(cur_object);
+        int bkind = pi(best.kind), bindex = pi(best.index), bobject = pi(best.object);
+        uint32_t brank = (uint32_t)pi((int)best.rank);
+        double bd = p64(best.d);
+        // frontier entry f of this half: row f / hs, column hb + f % hs of the wave's stack words
+        auto fr = [&](int f) -> uint32_t& {
+            return st_node[(f >> hshift) * 256 + (tid & ~63) + hb + (f & (hs - 1))];
+        };
+        const int cap = hs * STACK;
+        // a batch pushes at most 3 net entries per entry taken and stays below `safe`; above it, one
+        // entry per iteration is a depth-first walk of one subtree, which needs at most the per-lane
+        // walk's stack (< STACK) plus one word per level (it pushes every hit child), < 2 * STACK
+        const int safe = cap - 4 * STACK;
+        int32_t* const leaves = &wl_tri[wbase + (upper ? kWaveList / 2 : 0)];  // <= 4 per worker
+        static_assert(kWaveList / 2 >= 4 * 64, "each half of the wave FIFO holds a step's leaves");
+        if (r == 0) fr(0) = (uint32_t)pi(node);
+        int n = 1;  // this half's frontier size
+        while (true) {
+            const bool act = n > 0;
+            if (__ballot(act) == 0) break;
+            if (!act) continue;
+            VR_MARK("lone_step");
+#ifdef VR_COOP_PROF
+            cp_n[0]++;  // lone-walk iterations (per half)
+#endif
+            if (n > cap - 4) {  // cannot happen (above); a device error rather than a stray LDS write
+                atomicOr(A.error_flag, 1);
+                n = 0;
+                continue;
+            }
+            int t = n < hs ? n : hs;
+            if (n + 3 * t > safe) t = (safe - n) / 3 > 1 ? (safe - n) / 3 : 1;
+            const int my = r < t ? (int)fr(n - 1 - r) : -1;
+            n -= t;
+            uint32_t im = 0, lm = 0;
+            int c[4] = {0, 0, 0, 0};
+            int32_t le[4] = {0, 0, 0, 0};
+            if (my >= 0) {
+                const Node4& nd = node_at(my);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    c[k] = nd.child[k];
+                    float f, g;
+                    bool maybe, sure;
+                    slab32_flags(nd.box[k], ry, f, g, maybe, sure);
+                    const bool pass = c[k] != kEmptyChild && maybe && !(f > cf || g < cb);
+                    im |= (pass && c[k] >= 0) ? 1u << k : 0u;
+                    lm |= (pass && c[k] < 0) ? 1u << k : 0u;
+                    le[k] = (~c[k]) | ((pass && !sure) ? INT32_MIN : 0);
+                }
+            }
+            int nl = 0;  // hit leaves, in (child slot, worker) order
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool ih = (im >> k) & 1u, lh = (lm >> k) & 1u;
+                const uint64_t mi = __ballot(ih) & gmask, ml = __ballot(lh) & gmask;
+                if (ih) fr(n + (int)lanes_below(mi)) = (uint32_t)c[k];
+                if (lh) leaves[nl + (int)lanes_below(ml)] = le[k];
+                n += (int)__popcll(mi);
+                nl += (int)__popcll(ml);
+            }
+            for (int b = 0; b < nl; b += hs) {  // nl is uniform per half: the halves branch apart
+                VR_MARK("lone_leaf");
+#ifdef VR_COOP_PROF
+                cp_n[1]++;  // lone-walk leaf rounds (per half)
+#endif
+                const bool mine = r < nl - b;
+                double d = -1.0;
+                uint64_t key = 0;
+                if (mine) {
+                    const int e = leaves[b + r];
+                    const int tri = e & 0x7fffffff;
+                    const TriVerts tv = load_tri(tri_at(tri));
+                    double bb3[3];
+                    d = triangle_distance(tv, op, bb3);
+                    if (e < 0 && d >= 0.0) {  // the leaf's f32 box test was too close to call
+                        double bb[6], lo, hi;
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+                            bb[2 * a] = fmin(fmin(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                            bb[2 * a + 1] = fmax(fmax(tv.v[a], tv.v[3 + a]), tv.v[6 + a]);
+                        }
+                        if (!slab(bb, op, lo, hi)) d = -1.0;
+                    }
+                    key = ((uint64_t)(uint32_t)tv.rank << 32) | (uint32_t)tri;
+                }
+                const bool hit = mine && d >= 0.0;
+                const uint64_t hm = __ballot(hit) & gmask;
+                if (hm == 0) continue;
+                // the round's candidate over this half: the minimum distance (non-negative, so its
+                // bits order as integers), and at it the highest rank (its triangle in the low half);
+                // most rounds have one hit, taken by one permute
+                const uint64_t db = hit ? (uint64_t)__double_as_longlong(d) : ~0ull;
+                uint64_t dmin, kmax;
+                if (__popcll(hm) == 1) {
+                    const int src = (int)__builtin_ctzll(hm);
+                    dmin = __shfl(db, src);
+                    kmax = __shfl(key, src);
+                } else {
+                    dmin = db;
+                    for (int sh = hs >> 1; sh >= 1; sh >>= 1) {
+                        const uint64_t w = __shfl_xor(dmin, sh);
+                        dmin = w < dmin ? w : dmin;
+                    }
+                    kmax = hit && db == dmin ? key : 0ull;
+                    for (int sh = hs >> 1; sh >= 1; sh >>= 1) {
+                        const uint64_t w = __shfl_xor(kmax, sh);
+                        kmax = w > kmax ? w : kmax;
+                    }
+                }
+                const double dd = __longlong_as_double((long long)dmin);
+                const uint32_t rk = (uint32_t)(kmax >> 32);
+                // takes_hit for the owner
+                const bool closer = !bkind | (dd < bd);
+                const bool tie = (dd == bd) & ((bobject == cobj) ? (rk > brank) : (cobj < bobject));
+                if (closer | tie) {
+                    bd = dd;
+                    bkind = kTri;
+                    bindex = (int)(uint32_t)kmax;
+                    brank = rk;
+                    bobject = cobj;
+                    cf = round_away_f32(bd + S.margin * (1.0 + fabs(bd)) + margin_of(ry));  // set_cull_far
+                }
+            }
+        }
+        // each owner takes its half's results (from the half's first lane)
+        const int src = (two && (int)lane == ob) ? 32 : 0;
+        const double rd = __shfl(bd, src);
+        const int rkind = __shfl(bkind, src), rindex = __shfl(bindex, src), robject = __shfl(bobject, src);
+        const uint32_t rrank = (uint32_t)__shfl((int)brank, src);
+        const float rcf = __shfl(cf, src);
+        if ((own >> lane) & 1ull) {
+            best.d = rd;
+            best.kind = rkind;
+            best.index = rindex;
+            best.rank = rrank;
+            best.object = robject;
+            cull_far = rcf;
+            node = -1;
+            sp = 0;
+        }
+    };
     while (true) {
         // ---------------------------------------------------------------- phase A: shade
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
         // that only meet the plane or spheres), so those lanes do not idle through phase B
+#ifdef VR_COOP_PROF
+        cp_prev = __builtin_amdgcn_s_memtime();
+        if (coop_on) cp_n[2]++;
+#endif
         for (int rep = 0; rep < A.phase_a_reps; ++rep) {
             VR_MARK("phaseA_top");
             __builtin_amdgcn_s_setprio(kPrioA);
@@ -1006,6 +1233,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         if (lanes_ine(state, kDone) == 0) break;
         const bool tail = lanes_ieq(state, kDone) != 0;  // wave-uniform, fixed through phase B
         (void)tail;
+        VR_CP(0);
         // ---------------------------------------------------------------- phase B: traverse
 #if VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
         uint32_t wd = 0;
@@ -1040,7 +1268,27 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         coop_on = nlive >= 1 && nlive <= (int)A.coop &&
                                   (__ballot(state != kDone && bounces >= (int)A.coop_bounces) == live);
                     coop = coop_on && nlive >= 1;
-                    if (coop) coop_step(live);
+#ifdef VR_COOP_PROF
+                    if (!coop && nlive > (int)cp_maxlive) cp_maxlive = nlive;
+#endif
+                    VR_CP(3);
+#ifdef VR_COOP_PROF
+                    if (coop_on && cp_r0 == 0) cp_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+                    if (coop) {
+                        // the traversing paths' walks of their BVHs at once when nothing is pending
+                        const uint64_t busy = lanes_ieq(state, kTraversing);
+                        const uint64_t fresh = busy & lanes_ige(node, 0) & lanes_ieq(sp, 0) & lanes_ieq(np, 0);
+                        if (A.lone_walk && busy != 0 && fresh == busy && __popcll(busy) <= 2 && q_head == q_tail) {
+#ifdef VR_COOP_PROF
+                            cp_n[3]++;
+#endif
+                            lone_walk(busy);
+                        }
+                        else
+                            coop_step(live);
+                    }
+                    VR_CP(1);
                 }
             }
             if (COUNT) {  // how full this iteration's node step is (the headroom of merging waves)
@@ -1166,8 +1414,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     !room || at_node == 0) {
                     VR_SEC(0);
                     VR_MARK("leaf_test");
+                    VR_CP(3);
+#ifdef VR_COOP_PROF
+                    if (coop_on) cp_n[1]++;
+#endif
                     leaf_round(queued < 64u ? queued : 64u);
                     q_head = __builtin_amdgcn_readfirstlane(q_head + (queued < 64u ? queued : 64u));
+                    VR_CP(2);
                 }
             }
             VR_STAMP(4);
@@ -1177,9 +1430,38 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 ++bvh_i;
                 if (!start_bvhs()) state = kTraversed;
             }
+            VR_CP(3);
         } while (lanes_ieq(state, kTraversing) != 0 &&
                  __popcll(lanes_ieq(state, kTraversed)) < (int)A.shade_threshold);
     }
+#ifdef VR_COOP_PROF  // sums over the tail waves into the context's queue buffer, words 8..18 (vr_host.cpp prints them)
+    if (coop_on && lane == 0) {
+        unsigned long long* o = (unsigned long long*)A.queue + 8;
+        for (int i = 0; i < 4; ++i) atomicAdd(o + i, (unsigned long long)cp_t[i]);
+        for (int i = 0; i < 3; ++i) atomicAdd(o + 4 + i, (unsigned long long)cp_n[i]);
+        atomicAdd(o + 7, 1ull);
+        atomicMax(o + 8, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
+        atomicAdd(o + 10, (unsigned long long)cp_n[3]);
+        atomicAdd(o + 9, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
+    }
+    {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (now - cp_s > 100000 && lane == 0) {  // waves that ran for more than 1 ms: one record each
+            unsigned long long* o = (unsigned long long*)A.queue + 8;
+            const unsigned long long slot = atomicAdd(o + 11, 1ull);
+            if (slot < 1000) {
+                unsigned long long* r = o + 16 + 6 * slot;
+                r[0] = now - cp_s;
+                r[1] = coop_on ? now - cp_r0 : 0;
+                r[2] = cp_n[3];
+                r[3] = cp_n[2];
+                r[4] = cp_maxlive;
+                r[5] = cp_s;
+            }
+        }
+    }
+#endif
+#undef VR_CP
 
     if (COUNT) {
         atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
