@@ -14,11 +14,11 @@ from vanrijn_amd.render import Tile, render_tile_device  # noqa: E402
 
 def main():
     spp = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    which = sys.argv[2] if len(sys.argv) > 2 else "main"
+    which = sys.argv[2] if len(sys.argv) > 2 else "main"  # argv[3]: frame size (square)
     path = "/tmp/wg_times.bin"
     os.environ["VR_WG_TIMES_PATH"] = path
     ds = (scenes.main_scene() if which == "main" else scenes.bench_scene()).device_scene(0)
-    W = H = 1024
+    W = H = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
     state = torch.zeros(W * H * 8, dtype=torch.float64, device="cuda")
     st = render_tile_device(ds, Tile(0, W, 0, H), H, W, spp, 1, 0, state.data_ptr(),
                             torch.cuda.current_stream().cuda_stream, counters=True)
