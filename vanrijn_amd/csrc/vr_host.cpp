@@ -1066,8 +1066,8 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         const uint64_t lsamples = a.tile_width * a.tile_height * (uint64_t)p->spp;
         a.coop = (lsamples <= VR_COOP_SAMPLES && (s->mats & 2) && s->dark0) ? 2u : 0u;
         if (const char* co = tuning_env("VR_COOP")) a.coop = (uint32_t)std::min(2, std::max(0, atoi(co)));
-        a.coop_bounces = VR_COOP_BOUNCES;
-        a.lone_walk = 1;  // ... once every live path of the wave has bounced this often
+        a.coop_bounces = VR_COOP_BOUNCES;  // ... once every live path of the wave has bounced this often
+        a.lone_walk = 1;
         if (const char* cb = tuning_env("VR_COOP_BOUNCES")) a.coop_bounces = (uint32_t)std::max(0, atoi(cb));
     }
     {
