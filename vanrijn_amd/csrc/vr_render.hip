@@ -1874,16 +1874,19 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
 #endif
     // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
     // of scenes with a reflective material)
+#ifndef VR_COOP_MINW  // their waves per SIMD
+#define VR_COOP_MINW 2
+#endif
     const bool coop = c.coop;
     if (!c.dark0) {
         VR_MODES(false, 3);
     } else if (mats == 1) {
         VR_MODES(true, 1);
     } else if (mats == 2) {
-        if (coop) VR_K(STACK, false, false, true, 2, 3, false, true);
+        if (coop) VR_K(STACK, false, false, true, 2, VR_COOP_MINW, false, true);
         else VR_MODES(true, 2);
     } else {
-        if (coop) VR_K(STACK, false, false, true, 3, 3, false, true);
+        if (coop) VR_K(STACK, false, false, true, 3, VR_COOP_MINW, false, true);
         else VR_MODES(true, 3);
     }
 #undef VR_MODES
