@@ -870,9 +870,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // whole rest of each path's walk of its current BVH in one call.  With one owner every lane
     // works for it; with two the lower half works for the lower owner and the upper half for the
     // other, both walks at once.  An owner's frontier of nodes to visit is a LIFO over its half's
-    // columns of the wave's stack words; each iteration pops up to one entry per worker, tests the
-    // entries' children against the owner's ray, pushes the hit interior children and tests the hit
-    // leaves at once, one per worker per round.  The round's candidate (minimum distance, then the
+    // columns of the wave's stack words; each iteration pops up to one node per four workers, each
+    // worker tests one child box against the owner's ray, the hit interior children are pushed and
+    // the hit leaves tested at once, one per worker.  The round's candidate (minimum distance, then the
     // highest reference rank) is merged with takes_hit's rule, as in leaf_round, so each path gets
     // what its per-lane walk finds: only the visiting order differs.  Against coop_step it saves the
     // per-step owner-state permutes and stack remapping and the separate leaf rounds through the FIFO
@@ -934,36 +934,35 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 n = 0;
                 continue;
             }
-            int t = n < hs ? n : hs;
+            // four workers per node, one child each: a quarter of the per-worker instructions of
+            // one worker per node (C1 2.15 -> 1.60 ms, profiles/r05/lone/ab_split_c1.jsonl)
+            const int tw = hs >> 2;
+            int t = n < tw ? n : tw;
             if (n + 3 * t > safe) t = (safe - n) / 3 > 1 ? (safe - n) / 3 : 1;
-            const int my = r < t ? (int)fr(n - 1 - r) : -1;
+            const int slot = r >> 2, k = r & 3;
+            const int my = slot < t ? (int)fr(n - 1 - slot) : -1;
             n -= t;
-            uint32_t im = 0, lm = 0;
-            int c[4] = {0, 0, 0, 0};
-            int32_t le[4] = {0, 0, 0, 0};
+            bool ih = false, lh = false;
+            int c = 0;
+            int32_t le = 0;
             if (my >= 0) {
                 const Node4& nd = node_at(my);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    c[k] = nd.child[k];
-                    float f, g;
-                    bool maybe, sure;
-                    slab32_flags(nd.box[k], ry, f, g, maybe, sure);
-                    const bool pass = c[k] != kEmptyChild && maybe && !(f > cf || g < cb);
-                    im |= (pass && c[k] >= 0) ? 1u << k : 0u;
-                    lm |= (pass && c[k] < 0) ? 1u << k : 0u;
-                    le[k] = (~c[k]) | ((pass && !sure) ? INT32_MIN : 0);
-                }
+                c = nd.child[k];
+                float f, g;
+                bool maybe, sure;
+                slab32_flags(nd.box[k], ry, f, g, maybe, sure);
+                const bool pass = c != kEmptyChild && maybe && !(f > cf || g < cb);
+                ih = pass && c >= 0;
+                lh = pass && c < 0;
+                le = (~c) | ((pass && !sure) ? INT32_MIN : 0);
             }
-            int nl = 0;  // hit leaves, in (child slot, worker) order
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool ih = (im >> k) & 1u, lh = (lm >> k) & 1u;
+            int nl = 0;  // hit leaves, in (node, child slot) order
+            {
                 const uint64_t mi = __ballot(ih) & gmask, ml = __ballot(lh) & gmask;
-                if (ih) fr(n + (int)lanes_below(mi)) = (uint32_t)c[k];
-                if (lh) leaves[nl + (int)lanes_below(ml)] = le[k];
+                if (ih) fr(n + (int)lanes_below(mi)) = (uint32_t)c;
+                if (lh) leaves[(int)lanes_below(ml)] = le;
                 n += (int)__popcll(mi);
-                nl += (int)__popcll(ml);
+                nl = (int)__popcll(ml);
             }
             for (int b = 0; b < nl; b += hs) {  // nl is uniform per half: the halves branch apart
                 VR_MARK("lone_leaf");
@@ -1874,7 +1873,7 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
 #endif
     // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
     // of scenes with a reflective material)
-#ifndef VR_COOP_MINW  // their waves per SIMD
+#ifndef VR_COOP_MINW  // their waves per SIMD (2: no spills; C1 -9 %)
 #define VR_COOP_MINW 2
 #endif
     const bool coop = c.coop;
