@@ -81,33 +81,6 @@ __device__ inline uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// lane l's value, wave-uniform (v_readlane into SGPRs; l uniform)
-__device__ __forceinline__ int rl_i32(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rl_f32(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-__device__ __forceinline__ double rl_f64(double v, int l) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-// minimum / maximum of v over the wave's 64 lanes (all active), wave-uniform
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const uint64_t w = __shfl_xor(v, s);
-        v = w < v ? w : v;
-    }
-    return uniform64(v);
-}
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const uint64_t w = __shfl_xor(v, s);
-        v = w > v ? w : v;
-    }
-    return uniform64(v);
-}
-
 __host__ __device__ inline uint32_t tail_of(const RenderArgs& a) {
     return a.tail_samples < a.spp ? a.tail_samples : a.spp;
 }
