@@ -14,23 +14,31 @@ Workload (default --config c3 = BASELINE.json configs[2] / metric): the main.rs 
 (src/main.rs:120-189: plane, three spheres, Lambertian bunny; camera (-2, 1, -5)) at 1024x1024,
 256 samples per pixel per GPU.  The bunny OBJ is a Git-LFS pointer in the reference, so the mesh is
 the deterministic procedural stand-in (69,312 triangles, vanrijn_amd/scenes.py).  One "step" = one
-frame: rank r renders sample indices [(step*N + r)*spp, +spp) of the same image (weak scaling for
-c1-c3; c4 / c5 split ONE frame's 1024 / 256 spp over the N ranks, strong scaling), then the
+frame: rank r renders sample indices [(step*N + r)*spp, +spp) of the same image -- c3, c4 and c5
+split ONE frame's 256 / 1024 / 256 spp over the N ranks (strong scaling: the metric's "1024x1024
+@256spp, 1/2/4/8 GPUs" is a fixed workload), c1 / c2 give every rank a whole frame (weak) -- then the
 per-pixel sums {X, Y, Z, weight} (32 B) are summed onto rank 0 with one RCCL reduce over xGMI inside
-the timed region (vanrijn_amd/distributed.py frame_step, the same step the gloo tests run).
+the timed region (vanrijn_amd/distributed.py frame_step, the same step the gloo tests run).  At N > 1
+a split config also times every rank rendering the whole frame (`weak_scaling`, secondary), and rank 0
+runs the PMC passes on its own shard after the timed regions (`roofline`).
 
 Printed (rank 0, one JSON line):
   value       total samples of all ranks / max-over-ranks wall time of the timed steps;
   roofline    the render kernel against its binding ceiling, from rocprofv3 PMC passes run by this
               bench itself on this build and workload (live_pmc: child processes, one counter group
               each; the committed profiles/pmc_records.json only if they fail): VALU issue (f64-heavy
-              vector ALU) vs HBM.  `achieved` = VALU issue cycles per launch (the PMC instruction
-              mix x the issue cost of each class measured by tools/opcost.hip, profiles/r03/
-              opcost.json) / the live HIP-event kernel time; `hbm_frac` = PMC HBM bytes (2 FETCH_SIZE
-              + WRITE_SIZE) / kernel time / 8 TB/s; SURVEY.md 8(d)'s algorithmic-bytes formula is
-              kept as `algorithmic_*` (its bytes are served by L2 / MALL, not HBM, so its fraction is
-              no physical bound); lane utilisation and per-launch counters come from a counting
-              launch of the same workload and need no PMC;
+              vector ALU) vs HBM.  `achieved` = the SIMD-cycles the hardware spent issuing VALU per
+              launch (4 x SQ_ACTIVE_INST_VALU) / the live HIP-event kernel time, `peak` = 1024 SIMDs
+              x 2.4 GHz, `frac` = achieved / peak (measured, not priced); `useful_lane_frac` = frac x
+              the lane efficiency of what was issued; `valu_issue_frac_model` prices the PMC
+              instruction mix at the per-class issue costs tools/opcost.hip measured (profiles/r03/
+              opcost.json); `hbm_frac` = PMC HBM bytes (2 FETCH_SIZE + WRITE_SIZE) / kernel time /
+              8 TB/s; SURVEY.md 8(d)'s algorithmic-bytes formula is kept as `cache_served_*` (its
+              bytes are served by L2 / MALL, not HBM, so its fraction is no bound -- above 1 at C3);
+              lane utilisation and per-launch counters come from a counting launch of the same
+              workload and need no PMC;
+  traced_msamples_per_s  the samples actually traced per second (`value` also counts the samples of
+              frustum-culled 8x8 blocks, applied in closed form: `frustum_culled_sample_fraction`);
   scene_build vr_scene_create time (excluded from `value`, SURVEY.md 8(d));
   reduce      bytes and RCCL time per step of the cross-GPU reduce;
   drop_in     the reference's own call pattern (src/main.rs:197-216): host threads each calling
@@ -70,7 +78,9 @@ SEED = 0x5EED0001
 CONFIGS = {
     "c1": dict(scene="bench", width=256, height=256, spp=16, split=False),
     "c2": dict(scene="main", width=512, height=512, spp=64, split=False),
-    "c3": dict(scene="main", width=1024, height=1024, spp=256, split=False),
+    # the metric's own workload: ONE 1024^2 @256spp frame, its samples split over the 1/2/4/8 GPUs
+    # (strong scaling; the weak figure -- every rank a whole frame -- is the line's `weak_scaling`)
+    "c3": dict(scene="main", width=1024, height=1024, spp=256, split=True),
     "c4": dict(scene="main", width=2048, height=2048, spp=1024, split=True),
     "c5": dict(scene="c5", width=4096, height=4096, spp=256, split=True),
 }
@@ -229,6 +239,12 @@ def live_pmc(child_args, timeout_s=150):
     if not prof:
         return {"error": "rocprofv3 not found"}
     tmp = tempfile.mkdtemp(prefix="vr_pmc_")
+    # a one-process child even under torch.distributed.run (rank 0 at N > 1): no rank variables
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    env["TMPDIR"] = tmp
     per_launch, kernel_ns = {}, {}
     try:
         for name, counters in PMC_PASSES:
@@ -236,7 +252,7 @@ def live_pmc(child_args, timeout_s=150):
             cmd = [prof, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--pmc"] + counters + \
                   ["--", sys.executable, os.path.abspath(__file__), "--pmc-child"] + child_args
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True,
-                                 env=dict(os.environ, TMPDIR=tmp))
+                                 env=env)
             try:
                 rc = p.wait(timeout=timeout_s)
             except subprocess.TimeoutExpired:
@@ -268,10 +284,12 @@ def roofline(counts, pixels, kernel_s, key, passes=1, pmc=None):
     rates use the per-launch time kernel_s / passes.  `pmc`: this run's live PMC record, else the
     committed record of this library build (profiles/pmc_records.json)."""
     alg = algorithmic_bytes(counts, pixels)
+    # SURVEY.md 8(d)'s per-unit bytes x this launch's counts: served by L2 and the Infinity Cache
+    # (L2 hit rate 0.86 at C3), so their rate is no HBM bound -- it exceeds the HBM peak at C3
     r = {"kernel": "render_kernel", "kernel_ms": round(kernel_s * 1e3, 3), "launches_per_step": passes,
-         "algorithmic_bytes_per_launch": alg,
-         "algorithmic_gbs": round(alg / kernel_s / 1e9, 2),
-         "algorithmic_frac": round(alg / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+         "cache_served_algorithmic_bytes_per_launch": alg,
+         "cache_served_algorithmic_gbs": round(alg / kernel_s / 1e9, 2),
+         "cache_served_algorithmic_frac_of_hbm_peak": round(alg / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
          "layout_bytes_per_launch": layout_bytes(counts, pixels),
          "layout_gbs": round(layout_bytes(counts, pixels) / kernel_s / 1e9, 2),
          "counters_per_launch": {k: counts[k] for k in ("box_tests", "node_visits", "triangle_tests", "rays",
@@ -291,22 +309,31 @@ def roofline(counts, pixels, kernel_s, key, passes=1, pmc=None):
     traffic = 2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024  # gfx950: FETCH_SIZE counts 128-B lines at 64 B
     hbm_gbs = traffic / launch_s / 1e9
     valu = valu_issue_cycles(pmc, costs)
-    valu_rate = valu / launch_s / 1e9  # G SIMD-cycles of VALU issue per second
+    valu_rate = valu / launch_s / 1e9  # G SIMD-cycles of VALU issue per second (priced model)
     valu_peak = SIMDS * CLOCK_GHZ
     clk = pmc["GRBM_GUI_ACTIVE"] / 8 / (rec["kernel_ns"] * 1e-9) / 1e9  # effective clock of the profiled launch
-    fracs = {"valu": valu_rate / valu_peak, "hbm": hbm_gbs / HBM_PEAK_GBS}
+    # measured: the SIMD-cycles the hardware spent issuing VALU (SQ_ACTIVE_INST_VALU
+    # counts per SIMD-quad: x4), per second of the live kernel time -- the line's headline fraction
+    busy = 4 * pmc["SQ_ACTIVE_INST_VALU"] if pmc.get("SQ_ACTIVE_INST_VALU") else None
+    busy_rate = busy / launch_s / 1e9 if busy else None
+    lane_eff = pmc["SQ_THREAD_CYCLES_VALU"] / (64 * pmc["SQ_ACTIVE_INST_VALU"]) if busy else None
+    fracs = {"valu": (busy_rate if busy else valu_rate) / valu_peak, "hbm": hbm_gbs / HBM_PEAK_GBS}
     bound = max(fracs, key=fracs.get)
     r.update({
         "bound": bound,
-        "achieved": round(valu_rate, 2) if bound == "valu" else round(hbm_gbs, 2),
+        "achieved": round(busy_rate if busy else valu_rate, 2) if bound == "valu" else round(hbm_gbs, 2),
         "peak": valu_peak if bound == "valu" else HBM_PEAK_GBS,
-        "unit": "G VALU issue-cycles/s" if bound == "valu" else "GB/s",
+        "unit": ("G VALU-busy SIMD-cycles/s" if busy else "G VALU issue-cycles/s (priced)") if bound == "valu"
+        else "GB/s",
         "frac": round(fracs[bound], 4),
+        "frac_source": "hardware: 4 SQ_ACTIVE_INST_VALU / live kernel time / (1024 SIMDs x 2.4 GHz)" if busy
+        else "priced model (SQ_ACTIVE_INST_VALU not collected)",
+        "useful_lane_frac": round(fracs["valu"] * lane_eff, 4) if busy else None,
         "traffic": traffic,
         "hbm_gbs": round(hbm_gbs, 2), "hbm_frac": round(fracs["hbm"], 4),
-        "valu_issue_frac": round(fracs["valu"], 4),
-        # the same issue cycles against the profiled launch's own clock (DVFS holds it below 2.4 GHz)
-        "valu_issue_frac_at_profiled_clock": round(valu / (rec["kernel_ns"] * 1e-9) / (SIMDS * clk * 1e9), 4),
+        "valu_issue_frac_model": round(valu_rate / valu_peak, 4),
+        # the priced issue cycles against the profiled launch's own clock (DVFS holds it below 2.4 GHz)
+        "valu_issue_frac_model_at_profiled_clock": round(valu / (rec["kernel_ns"] * 1e-9) / (SIMDS * clk * 1e9), 4),
         "valu_issue_cycles_per_launch": valu,
         "valu_cost_model_cycles": {k: round(v, 3) for k, v in costs.items()},
         "valu_cost_source": os.path.relpath(OPCOST_PATH, ROOT) + " (tools/opcost.hip, 3 waves/SIMD)",
@@ -435,8 +462,9 @@ def drop_in_leg(dscene, width, height, frames, threads, device):
     assert merged == frames and float(image.weight_buffer.min()) == frames
     return {"value": round(frames * width * height / dt / 1e6, 3), "unit": "Msamples/s", "threads": threads,
             "frames": frames, "ms_per_frame": round(dt / frames * 1e3, 3),
-            "pattern": "main.rs:197-216: worker threads x vr_partial_render_scene (1 spp, full frame, host "
-                       "buffers: 88 B/pixel back over PCIe), vr_merge_tile on the main thread"}
+            "pattern": "main.rs:197-216: worker threads x vr_partial_render_scene (1 spp, full frame into a "
+                       "fresh host buffer: only colour_sum, 24 B/pixel, crosses PCIe; the host derives the "
+                       "other 64 B/pixel of the 88-B AccumulationBuffer layout), vr_merge_tile on the main thread"}
 
 
 # ---------------------------------------------------------------------------- rank launcher
@@ -577,57 +605,71 @@ def main():
     state = torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}")
     stream = torch.cuda.current_stream()
 
-    reduce_events = []
-
-    def step(i, timed=False, defer=False):
+    def step(i, spp_r, timer=None, timed=False, defer=False):
         # defer: the render's HIP events are recorded but not waited for (VR_LAUNCH_DEFER_TIMES), so
         # back-to-back timed frames queue without a host round trip between them; their times are
         # collected after the timed region
         def shard(first, st):
-            return render_tile_device(dscene, tile, H, W, spp, SEED, first, st.data_ptr(), stream.cuda_stream,
+            return render_tile_device(dscene, tile, H, W, spp_r, SEED, first, st.data_ptr(), stream.cuda_stream,
                                       timed=timed and not defer, defer_times=defer, device=local)
-        return D.frame_step(shard, state, i, spp, timer=reduce_events if timed or defer else None)
+        return D.frame_step(shard, state, i, spp_r, timer=timer)
+
+    def timed_region(spp_r, first_step):
+        """args.warmup untimed + args.steps timed frames of spp_r samples per pixel on every rank,
+        bracketed by barrier + synchronize; the max over ranks of the wall time, and this rank's
+        HIP-event kernel times."""
+        for i in range(args.warmup):
+            step(first_step + i, spp_r)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        events = []
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(first_step + args.warmup + i, spp_r, timer=events, defer=True)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        stream_check_error(dscene, stream.cuda_stream, device=local)  # device errors of the untimed steps
+        # the timed frames' HIP-event times (render kernel on the launch stream; the ordered per-pixel
+        # Kahan reduce after it), and their device errors
+        lt = collect_launch_times(dscene, stream.cuda_stream, device=local)
+        assert lt["launches"] == args.steps, lt
+        if distributed:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return {"elapsed": elapsed, "kernel_s": lt["kernel_ms"] / args.steps / 1e3,
+                "reduce_ms": lt["reduce_ms"] / args.steps, "passes": max(1, lt["max_passes"]),
+                "rccl_ms": [a.elapsed_time(b) for a, b in events]}
 
     if args.pmc_child:  # under rocprofv3 (live_pmc): one timed frame of the workload, nothing else
-        step(1, timed=True)
+        step(1, spp, timed=True)
         torch.cuda.synchronize()
         return
     progress(f"scene built in {build_s:.3f} s; counting launch")
-    # counting launch (untimed): traversal counters of exactly this workload
+    # counting launch (untimed): traversal counters of exactly this rank's workload
     counts = render_tile_device(dscene, tile, H, W, spp, SEED, rank * spp, state.data_ptr(), stream.cuda_stream,
                                 counters=True, device=local)
-    for i in range(args.warmup):
-        step(1 + i)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(1 + args.warmup + i, defer=True)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    stream_check_error(dscene, stream.cuda_stream, device=local)  # device errors of the untimed steps
-    # the timed frames' HIP-event times (render kernel on the launch stream; the ordered per-pixel
-    # Kahan reduce after it), and their device errors
-    lt = collect_launch_times(dscene, stream.cuda_stream, device=local)
-    assert lt["launches"] == args.steps, lt
-    kernel_ms = [lt["kernel_ms"] / args.steps]
-    reduce_ms = [lt["reduce_ms"] / args.steps]
-    passes = [max(1, lt["max_passes"])]  # launches per frame (staging cap)
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    tr = timed_region(spp, 1)
+    elapsed = tr["elapsed"]
     progress(f"timed {args.steps} steps: {elapsed / args.steps * 1e3:.3f} ms/step")
-    rccl_ms = [a.elapsed_time(b) for a, b in reduce_events]
+    rccl_ms = tr["rccl_ms"]
     samples = world * args.steps * W * H * spp
     value = samples / elapsed / 1e6
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    avg_kernel_s = tr["kernel_s"]
+    weak = None
+    if world > 1 and cfg["split"]:
+        # secondary: every rank renders the whole frame's spp (weak scaling), after the headline region
+        wr = timed_region(cfg["spp"], 1 + 2 * (args.warmup + args.steps))
+        weak = {"value": round(world * args.steps * W * H * cfg["spp"] / wr["elapsed"] / 1e6, 3),
+                "unit": "Msamples/s", "ms_per_step": round(wr["elapsed"] / args.steps * 1e3, 3),
+                "spp_per_gpu": cfg["spp"], "render_kernel_ms": round(wr["kernel_s"] * 1e3, 3),
+                "scaling": "weak"}
+        progress(f"weak: {weak['ms_per_step']} ms/step")
     workload = {"main": f"main.rs scene (plane, 3 spheres, Lambertian bunny), {W}x{H}",
                 "bench": f"bench scene (reflective bunny), {W}x{H}",
                 "c5": f"C5: main.rs plane + spheres + 1,051,392-triangle synthetic mesh, {W}x{H}"}[cfg["scene"]]
@@ -655,23 +697,29 @@ def main():
                    "parallelism": f"spp-split x{world}, RCCL reduce",
                    "pmc_key": config_key(cfg["scene"], W, H, spp)},
     }
+    # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied
+    # as the photon {0, 0} without tracing: the records are bit-identical with VR_LAUNCH_NO_CULL
+    # (tests/test_gpu_cull.py); every sample is counted in `value`, the traced ones here
+    out["traced_msamples_per_s"] = round(world * args.steps * counts["samples"] / elapsed / 1e6, 3)
+    if weak:
+        out["weak_scaling"] = weak
     pmc = None
-    if rank == 0 and world == 1 and not args.no_pmc:
-        child = ["--config", args.config, "--width", str(W), "--height", str(H), "--spp", str(cfg["spp"]),
+    if rank == 0 and not args.no_pmc:
+        # this rank's shard (at N > 1 too: the PMC child is a one-process run of the same spp)
+        child = ["--config", args.config, "--width", str(W), "--height", str(H), "--spp", str(spp),
                  "--scene", cfg["scene"]] + (["--mesh", args.mesh] if args.mesh else []) + \
                 (["--host-build"] if args.host_build else [])
         pmc = live_pmc(child)
-    out["roofline"] = roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), max(passes), pmc)
+    out["roofline"] = roofline(counts, W * H, avg_kernel_s, config_key(cfg["scene"], W, H, spp), tr["passes"], pmc)
+    if world > 1:
+        out["roofline"]["shard"] = f"rank 0's {spp} spp of the {cfg['spp'] if cfg['split'] else spp * world} spp frame"
     out["scene_build"] = build
     # the path's one exchange: {sum X, Y, Z, weight} of every pixel, 32 B, reduced
     # onto rank 0 inside the timed step (RCCL; under torch.distributed.run also at world size 1)
     out["reduce"] = {"collective": "dist.reduce(SUM, f64) onto rank 0" if distributed else "none (one process)",
                      "bytes_per_step_per_rank": D.reduce_bytes(state) if distributed else 0,
                      "ms_per_step": round(sum(rccl_ms) / len(rccl_ms), 3) if rccl_ms else 0.0}
-    out["roofline"]["reduce_kernel_ms"] = round(sum(reduce_ms) / len(reduce_ms), 3)
-    # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied
-    # as the photon {0, 0} without tracing: the records are bit-identical with VR_LAUNCH_NO_CULL
-    # (tests/test_gpu_cull.py); every sample is counted in `value`
+    out["roofline"]["reduce_kernel_ms"] = round(tr["reduce_ms"], 3)
     out["roofline"]["frustum_culled_sample_fraction"] = round(1.0 - counts["samples"] / (W * H * spp), 4)
     if rank == 0 and world == 1 and not args.no_drop_in:
         progress("drop-in leg")
@@ -685,6 +733,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:
+        dist.barrier()  # the other ranks wait for rank 0's PMC passes before the group goes away
         dist.destroy_process_group()
 
 

@@ -230,7 +230,10 @@ typedef struct vr_accumulation_buffer {
 
 /* Sampling parameters.  Each (pixel, sample) draws its random numbers from the counter-based
  * stream (seed, row*width+column, first_sample + s) ("vr-hash32 v2"), so results do
- * not depend on tiling, launch split or device count. */
+ * not depend on tiling, launch split or device count.  The stream's index space is 2^32 pixels x 2^32
+ * samples: width*height > 2^32 or first_sample + spp > 2^32 returns VR_ERROR_UNSUPPORTED.  Each 64-bit
+ * draw is two 32-bit hashes of one 32-bit counter word, so it carries 32 bits of state (a Standard
+ * f64 takes one of at most 2^32 values). */
 typedef struct vr_render_params {
     vr_tile tile;
     uint64_t height, width; /* full image, as partial_render_scene's height/width */
@@ -291,7 +294,7 @@ typedef struct vr_launch_stats {
 #define VR_LAUNCH_NO_CULL 8u
 /* no BVH distance culling: every box the ray's line crosses is walked (the reference's exhaustive
  * traversal, bounding_volume_hierarchy.rs:94-120), with the same records bit for bit -- the check
- * that the tie rule does not lean on the culling order (tests/test_gpu_nocull_ties.py; ABI 8) */
+ * that the tie rule does not lean on the culling order (tests/test_gpu_launch_variants.py; ABI 8) */
 #define VR_LAUNCH_NO_DIST_CULL 16u
 /* no cooperative tail (small launches of scenes with a reflective material otherwise spread a
  * wave's last one or two paths over its lanes): the same records bit for bit (ABI 8) */

@@ -97,6 +97,34 @@ def test_sharded_frame_matches_single_process(tmp_path, world, split):
     assert np.abs(cont["colour"] - both["colour"]).max() < 1e-12
 
 
+def test_c3_frame_is_split_over_the_ranks(tmp_path):
+    """bench.py's headline config (c3: one 1024^2 @256spp frame, 1/2/4/8 GPUs) is strong-scaled: at
+    world size 2 each rank renders 128 of the frame's 256 spp, and rank 0's reduced records equal one
+    process rendering all 256 -- exact weights, means within 1e-12 (src/main.rs:194-211's
+    rayon split).  The frame is shrunk to H x W pixels for the oracle; the spp are c3's."""
+    import importlib.util
+    from oracle import oracle_ffi as O
+    from vanrijn_amd.render import Tile
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    c3 = bench.CONFIGS["c3"]
+    assert c3["split"] and c3["spp"] == 256 and (c3["width"], c3["height"]) == (1024, 1024)
+    assert [D.shard_spp(c3["spp"], n, c3["split"]) for n in (1, 2, 4, 8)] == [256, 128, 64, 32]
+    out = str(tmp_path / "rank0.npy")
+    mp.spawn(_worker, args=(2, _free_port(), c3["spp"], c3["split"], 1, out), nprocs=2, join=True)
+    reduced = np.load(out)
+    firsts = sorted(int(f[-1]) for f in np.load(out + ".firsts.npy"))
+    assert firsts == [0, 128]  # 128 + 128: the two halves of one frame's sample range
+    orc = O.OracleScene(_small_scene().spec())
+    single = _records(orc.render_tile(Tile(0, W, 0, H), H, W, 256, seed=SEED, first_sample=0, mode=O.MODE_PRUNED))
+    fr, fs = R.fields(reduced, (H, W)), R.fields(single, (H, W))
+    assert np.array_equal(fr["weight"], fs["weight"]) and float(fr["weight"].min()) == 256.0
+    mean_r = D.mean_colour(torch.from_numpy(reduced)).numpy()
+    mean_s = D.mean_colour(torch.from_numpy(single)).numpy()
+    assert np.abs(mean_r - mean_s).max() < 1e-12
+
+
 def test_first_sample_partition():
     seen = set()
     for step in range(3):

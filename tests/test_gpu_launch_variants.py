@@ -116,6 +116,56 @@ def test_cooperative_tail_matches_the_oracle_on_a_crop(oracle):
     assert np.array_equal(img.weight_buffer, refi["weight"])
 
 
+def _two_mirror_scene():
+    """Two reflective bunny-like meshes side by side (two mesh BVHs; the second one's root is not node
+    0), close enough that paths bounce between them: the cooperative tail's owners then walk either
+    BVH from lanes other than 0 / 32 (a walk that starts at the wrong node, or at the
+    first BVH's root, is invisible on bench_scene's single mesh)."""
+    from vanrijn_amd.scene import (BoundingVolumeHierarchy, ColourRgbF, Mesh, NamedColour, ReflectiveMaterial, Scene,
+                                   Spectrum)
+    objs = []
+    for centre, seed, colour in (((-2.55, -0.5, 0.0), 0xB0BB1E, NamedColour.Yellow),
+                                 ((-0.95, -0.35, 0.25), 0xC0FFEE, NamedColour.Red)):
+        v, n = scenes.displaced_mesh(20, scenes._BUNNY_BUMPS, noise_seed=seed, noise_count=24, noise_amp=0.05,
+                                     scale=(0.8, 0.75, 0.8), centre=centre)
+        mat = ReflectiveMaterial(Spectrum.reflection_from_linear_rgb(ColourRgbF.from_named(colour)), 0.05, 0.9)
+        objs.append(BoundingVolumeHierarchy.build(Mesh(v, n, mat)))
+    return Scene(scenes.CAMERA_LOCATION, objs)
+
+
+def test_cooperative_tail_two_mirror_meshes(oracle):
+    """The cooperative tail on a scene of two mirror meshes: whole walks (lone_walk), per-step walks
+    (coop_step) and the plain kernel give the same records bit for bit, fresh and accumulating, the
+    COOP kernel is the one reported, and a crop where paths run long matches the oracle."""
+    scene = _two_mirror_scene()
+    ds = scene.device_scene(0)
+    H = W = 160
+    t = Tile(0, W, 0, H)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = []
+    for coop, lone in ((True, True), (True, False), (False, True)):
+        st = torch.zeros(H * W * 8, dtype=torch.float64, device="cuda")
+        s1 = render_tile_device(ds, t, H, W, 16, 0x5EED0001, 0, st.data_ptr(), stream, coop=coop, lone_walk=lone)
+        s2 = render_tile_device(ds, t, H, W, 5, 0x5EED0001, 16, st.data_ptr(), stream, accumulate=True, coop=coop,
+                                lone_walk=lone)
+        torch.cuda.synchronize()
+        assert bool(s1["variant"] & N.VARIANT_COOP) == coop and bool(s2["variant"] & N.VARIANT_COOP) == coop
+        out.append(st.cpu())
+    for o in out[1:]:
+        assert torch.equal(out[0].view(torch.int64), o.view(torch.int64))
+    assert np.isfinite(out[0].numpy()).all()
+    # against the oracle where the two meshes face each other, per sample (decisions) and as an image
+    orc = oracle.OracleScene(scene.spec())
+    crop = Tile(56, 104, 72, 120)
+    ref = orc.render_samples(crop, H, W, 4, seed=0x5EED0001, mode=oracle.MODE_PRUNED, nthreads=8)
+    assert (ref["bounces"] >= 8).sum() > 0  # some paths bounce between the mirrors
+    img = render_tile(ds, crop, H, W, 16, seed=0x5EED0001)
+    refi = orc.render_tile(crop, H, W, 16, seed=0x5EED0001, mode=oracle.MODE_PRUNED, nthreads=8)
+    assert np.linalg.norm(img.colour_buffer - refi["colour"], axis=2).max() < 1e-5
+    assert np.array_equal(img.weight_buffer, refi["weight"])
+    _decisions_equal(render_samples(ds, crop, H, W, 4, seed=0x5EED0001), ref)
+
+
 @pytest.mark.parametrize("which", ["main", "bench", "whitted", "materials"])
 def test_wide_offset_kernels_are_bit_identical(which):
     """The 64-bit-offset kernels (forced) render the same records as the default ones, and the launch

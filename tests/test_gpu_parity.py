@@ -211,6 +211,22 @@ def test_invalid_tile_is_an_error(main_pair):
         render_tile(scene, Tile(0, 10, 0, 10), 8, 8, 1, seed=1)
 
 
+def test_random_stream_index_space_is_enforced(main_pair):
+    """The stream base mix64(key ^ (pixel << 32 | sample)) is injective only below 2^32 pixels and
+    samples: sample ranges past 2^32 and images of more than 2^32
+    pixels are refused, the last representable sample renders."""
+    from vanrijn_amd._native import VrError
+    scene, _ = main_pair
+    t = Tile(0, 4, 0, 4)
+    with pytest.raises(VrError) as e:
+        render_tile(scene, t, 8, 8, 2, seed=1, first_sample=(1 << 32) - 1)
+    assert e.value.code == -7  # VR_ERROR_UNSUPPORTED
+    with pytest.raises(VrError):
+        render_tile(scene, t, 1 << 17, 1 << 16, 1, seed=1)
+    ok = render_tile(scene, t, 8, 8, 1, seed=1, first_sample=(1 << 32) - 1)
+    assert np.array_equal(ok.weight_buffer, np.ones((4, 4)))
+
+
 def test_full_size_properties(bench_pair):
     """Bench config size (1024^2) at low spp: invariances that hold at any size."""
     scene, _ = bench_pair

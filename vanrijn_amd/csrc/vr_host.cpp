@@ -987,6 +987,13 @@ int check_render_params(const vr_scene* s, const vr_render_params* p) {
     if (t.end_column < t.start_column || t.end_row < t.start_row || t.end_column > p->width ||
         t.end_row > p->height || p->width == 0 || p->height == 0)
         return fail(VR_ERROR_INVALID_ARGUMENT, "tile outside the image");
+    // the random stream's base mix64(key ^ (pixel << 32 | sample)) is injective
+    // only for pixel and sample indices below 2^32: a larger index would silently carry into the
+    // other field and repeat another (pixel, sample)'s stream
+    if (p->width > (1ull << 32) || p->height > (1ull << 32) || p->width * p->height > (1ull << 32))
+        return fail(VR_ERROR_UNSUPPORTED, "image of more than 2^32 pixels (random stream index space)");
+    if ((uint64_t)p->first_sample + p->spp > (1ull << 32) || (uint64_t)p->first_sample >= (1ull << 32))
+        return fail(VR_ERROR_UNSUPPORTED, "sample indices past 2^32 (random stream index space)");
     if (stack_depth(s) > 48 || wide_stack_depth(s) > 48)
         return fail(VR_ERROR_UNSUPPORTED, "BVH deeper than the largest traversal stack (48)");
     return VR_OK;
@@ -1792,7 +1799,7 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         a.staging = (double*)c->staging;
         if (launch_flags & VR_LAUNCH_NO_DIST_CULL) {
             // every box the line crosses is walked (culled() / cull_far / cull_behind never prune):
-            // the records stay the same bit for bit (tests/test_gpu_nocull_ties.py)
+            // the records stay the same bit for bit (tests/test_gpu_launch_variants.py)
             a.scene.margin = INFINITY;
             a.scene.behind_margin = INFINITY;
         }

@@ -138,6 +138,35 @@ __device__ __forceinline__ KArgs kargs() {
 
 enum LaneState : int { kNeedRay = 0, kTraversing = 1, kTraversed = 2, kDone = 3, kRayReady = 4 };
 
+#ifdef VR_COOP_PROF
+// VR_CP_DUMP (analysis builds): a tail wave's phase sums into words 8..18 of the context's queue
+// buffer, and one record per wave that ran for more than 1 ms (vr_host.cpp prints both)
+__device__ void coop_prof_dump(unsigned long long* o, bool coop_on, unsigned lane, const uint64_t* cp_t,
+                               const uint32_t* cp_n, uint64_t cp_r0, uint64_t cp_s, uint32_t cp_maxlive) {
+    if (coop_on && lane == 0) {
+        for (int i = 0; i < 4; ++i) atomicAdd(o + i, (unsigned long long)cp_t[i]);
+        for (int i = 0; i < 3; ++i) atomicAdd(o + 4 + i, (unsigned long long)cp_n[i]);
+        atomicAdd(o + 7, 1ull);
+        atomicMax(o + 8, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
+        atomicAdd(o + 10, (unsigned long long)cp_n[3]);
+        atomicAdd(o + 9, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
+    }
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (now - cp_s > 100000 && lane == 0) {
+        const unsigned long long slot = atomicAdd(o + 11, 1ull);
+        if (slot < 1000) {
+            unsigned long long* r = o + 16 + 6 * slot;
+            r[0] = now - cp_s;
+            r[1] = coop_on ? now - cp_r0 : 0;
+            r[2] = cp_n[3];
+            r[3] = cp_n[2];
+            r[4] = cp_maxlive;
+            r[5] = cp_s;
+        }
+    }
+}
+#endif
+
 // MATS: material kinds present (1 Lambertian, 2 reflective, 3 both); code for absent kinds is
 // compiled out, which keeps the reflective BSDF's acos/pow/exp off Lambertian-only scenes.
 // WHITTED: the WhittedIntegrator (whitted_integrator.rs:20-87) instead of SimpleRandomIntegrator.
@@ -197,10 +226,18 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         tprev = t_;                                           \
     }
     uint32_t samples_done = 0;
-#ifdef VR_COOP_PROF  // analysis builds: where a cooperative-tail wave's time goes (printf at its end)
-    uint64_t cp_t[4] = {0, 0, 0, 0}, cp_prev = 0;  // phase A, coop steps, leaf rounds, rest of phase B
-    uint32_t cp_n[4] = {0, 0, 0, 0};               // phase B iterations, leaf rounds, phase A entries, lone walks
-    uint64_t cp_r0 = 0;                            // s_memrealtime (100 MHz) when the wave's tail began
+    // The cooperative tail's profile (analysis builds, -DVR_COOP_PROF: where a tail wave's time goes;
+    // vr_host.cpp prints the sums after the launch).  One macro family, empty in every other build:
+    //   VR_CP(i)        s_memtime since the last stamp into phase i (0 phase A, 1 coop steps, 2 leaf
+    //                   rounds, 3 the rest of phase B), in tail waves;
+    //   VR_CPN(i, c)    event count i when c (0 lone-walk iterations, 1 leaf rounds, 2 phase A
+    //                   entries, 3 lone walks);
+    //   VR_CP_PHASE_A() phase A starts;  VR_CP_TAIL(n) the wave's live paths before its tail and the
+    //                   tail's start time;  VR_CP_DUMP() the wave's records at its end
+#ifdef VR_COOP_PROF
+    uint64_t cp_t[4] = {0, 0, 0, 0}, cp_prev = 0;
+    uint32_t cp_n[4] = {0, 0, 0, 0};
+    uint64_t cp_r0 = 0;  // s_memrealtime (100 MHz) when the wave's tail began
     const uint64_t cp_s = __builtin_amdgcn_s_memrealtime();
     uint32_t cp_maxlive = 0;
 #define VR_CP(i)                                              \
@@ -209,8 +246,21 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         cp_t[i] += t_ - cp_prev;                              \
         cp_prev = t_;                                         \
     }
+#define VR_CPN(i, c) \
+    if (c) cp_n[i]++;
+#define VR_CP_PHASE_A()                          \
+    cp_prev = __builtin_amdgcn_s_memtime();      \
+    VR_CPN(2, coop_on)
+#define VR_CP_TAIL(n)                                                           \
+    if (!coop && (n) > (int)cp_maxlive) cp_maxlive = (n);                      \
+    if (coop_on && cp_r0 == 0) cp_r0 = __builtin_amdgcn_s_memrealtime();
+#define VR_CP_DUMP() coop_prof_dump((unsigned long long*)A.queue + 8, coop_on, lane, cp_t, cp_n, cp_r0, cp_s, cp_maxlive)
 #else
 #define VR_CP(i)
+#define VR_CPN(i, c)
+#define VR_CP_PHASE_A()
+#define VR_CP_TAIL(n)
+#define VR_CP_DUMP()
 #endif
     if (COUNT && A.wg_times && tid == 0) A.wg_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const uint32_t bw = (uint32_t)((A.tile_width + 7) / 8), bh = (uint32_t)((A.tile_height + 7) / 8);
@@ -760,25 +810,28 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         uint32_t im = 0;                     // hit interior children
         int c[4] = {0, 0, 0, 0};
         int pos = o_sp;
+        // the owner's ray and cull bounds, permuted with the whole wave active: `work` differs between
+        // the halves, and the upper half's owner may be a lane of the lower half (ds_bpermute reads 0
+        // from a source lane outside exec)
+        Ray32 ry;
+        ry.ox = __shfl(pre32.ox, owner);
+        ry.oy = __shfl(pre32.oy, owner);
+        ry.oz = __shfl(pre32.oz, owner);
+        ry.ix = __shfl(pre32.ix, owner);
+        ry.iy = __shfl(pre32.iy, owner);
+        ry.iz = __shfl(pre32.iz, owner);
+        ry.nx = __shfl(pre32.nx, owner);
+        ry.ny = __shfl(pre32.ny, owner);
+        ry.nz = __shfl(pre32.nz, owner);
+        ry.e2 = __shfl(pre32.e2, owner);
+        const float cf = __shfl(cull_far, owner);
+        const float cb = __shfl(cull_behind, owner);
         if (work) {
             VR_MARK("coop_step");
             const int first_stack = o_node >= 0 ? 1 : 0;  // worker 0 takes the current node
             int my = -1;
             if (r < t) my = (r < first_stack) ? o_node : (int)st_node[coop_vaddr(owner, om, o_sp - 1 - (r - first_stack))];
             pos = o_sp - (t - first_stack);  // stack entries left below the taken ones
-            Ray32 ry;                        // the owner's ray and cull bounds
-            ry.ox = __shfl(pre32.ox, owner);
-            ry.oy = __shfl(pre32.oy, owner);
-            ry.oz = __shfl(pre32.oz, owner);
-            ry.ix = __shfl(pre32.ix, owner);
-            ry.iy = __shfl(pre32.iy, owner);
-            ry.iz = __shfl(pre32.iz, owner);
-            ry.nx = __shfl(pre32.nx, owner);
-            ry.ny = __shfl(pre32.ny, owner);
-            ry.nz = __shfl(pre32.nz, owner);
-            ry.e2 = __shfl(pre32.e2, owner);
-            const float cf = __shfl(cull_far, owner);
-            const float cb = __shfl(cull_behind, owner);
             if (my >= 0) {
                 const Node4& nd = node_at(my);
                 if (COUNT) cnt.node_visits++;
@@ -892,16 +945,18 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         const int safe = cap - 4 * STACK;
         int32_t* const leaves = &wl_tri[wbase + (upper ? kWaveList / 2 : 0)];  // <= 4 per worker
         static_assert(kWaveList / 2 >= 4 * 64, "each half of the wave FIFO holds a step's leaves");
-        if (r == 0) fr(0) = (uint32_t)pi(node);
+        // the owner's current node, permuted with the whole wave active: ds_bpermute reads 0 from a
+        // source lane outside exec, so a permute inside `r == 0` (lanes 0 / 32 only) would start
+        // the walk at node 0 whenever the owner is another lane
+        const int start = pi(node);
+        if (r == 0) fr(0) = (uint32_t)start;
         int n = 1;  // this half's frontier size
         while (true) {
             const bool act = n > 0;
             if (__ballot(act) == 0) break;
             if (!act) continue;
             VR_MARK("lone_step");
-#ifdef VR_COOP_PROF
-            cp_n[0]++;  // lone-walk iterations (per half)
-#endif
+            VR_CPN(0, true);  // lone-walk iterations (per half)
             if (n > cap - 4) {  // cannot happen (above); a device error rather than a stray LDS write
                 atomicOr(A.error_flag, 1);
                 n = 0;
@@ -939,9 +994,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             }
             for (int b = 0; b < nl; b += hs) {  // nl is uniform per half: the halves branch apart
                 VR_MARK("lone_leaf");
-#ifdef VR_COOP_PROF
-                cp_n[1]++;  // lone-walk leaf rounds (per half)
-#endif
+                VR_CPN(1, true);  // lone-walk leaf rounds (per half)
                 const bool mine = r < nl - b;
                 double d = -1.0;
                 uint64_t key = 0;
@@ -1022,10 +1075,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // ---------------------------------------------------------------- phase A: shade
         // repeated while some lane's new ray was resolved without BVH work (sky misses, rays
         // that only meet the plane or spheres), so those lanes do not idle through phase B
-#ifdef VR_COOP_PROF
-        cp_prev = __builtin_amdgcn_s_memtime();
-        if (coop_on) cp_n[2]++;
-#endif
+        VR_CP_PHASE_A();
         for (int rep = 0; rep < A.phase_a_reps; ++rep) {
             VR_MARK("phaseA_top");
             __builtin_amdgcn_s_setprio(kPrioA);
@@ -1240,21 +1290,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         coop_on = nlive >= 1 && nlive <= (int)A.coop &&
                                   (__ballot(state != kDone && bounces >= (int)A.coop_bounces) == live);
                     coop = coop_on && nlive >= 1;
-#ifdef VR_COOP_PROF
-                    if (!coop && nlive > (int)cp_maxlive) cp_maxlive = nlive;
-#endif
                     VR_CP(3);
-#ifdef VR_COOP_PROF
-                    if (coop_on && cp_r0 == 0) cp_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
+                    VR_CP_TAIL(nlive);
                     if (coop) {
                         // the traversing paths' walks of their BVHs at once when nothing is pending
                         const uint64_t busy = lanes_ieq(state, kTraversing);
                         const uint64_t fresh = busy & lanes_ige(node, 0) & lanes_ieq(sp, 0) & lanes_ieq(np, 0);
                         if (A.lone_walk && busy != 0 && fresh == busy && __popcll(busy) <= 2 && q_head == q_tail) {
-#ifdef VR_COOP_PROF
-                            cp_n[3]++;
-#endif
+                            VR_CPN(3, true);
                             lone_walk(busy);
                         }
                         else
@@ -1387,9 +1430,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     VR_SEC(0);
                     VR_MARK("leaf_test");
                     VR_CP(3);
-#ifdef VR_COOP_PROF
-                    if (coop_on) cp_n[1]++;
-#endif
+                    VR_CPN(1, coop_on);
                     leaf_round(queued < 64u ? queued : 64u);
                     q_head = __builtin_amdgcn_readfirstlane(q_head + (queued < 64u ? queued : 64u));
                     VR_CP(2);
@@ -1406,34 +1447,12 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         } while (lanes_ieq(state, kTraversing) != 0 &&
                  __popcll(lanes_ieq(state, kTraversed)) < (int)A.shade_threshold);
     }
-#ifdef VR_COOP_PROF  // sums over the tail waves into the context's queue buffer, words 8..18 (vr_host.cpp prints them)
-    if (coop_on && lane == 0) {
-        unsigned long long* o = (unsigned long long*)A.queue + 8;
-        for (int i = 0; i < 4; ++i) atomicAdd(o + i, (unsigned long long)cp_t[i]);
-        for (int i = 0; i < 3; ++i) atomicAdd(o + 4 + i, (unsigned long long)cp_n[i]);
-        atomicAdd(o + 7, 1ull);
-        atomicMax(o + 8, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
-        atomicAdd(o + 10, (unsigned long long)cp_n[3]);
-        atomicAdd(o + 9, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_r0));
-    }
-    {
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (now - cp_s > 100000 && lane == 0) {  // waves that ran for more than 1 ms: one record each
-            unsigned long long* o = (unsigned long long*)A.queue + 8;
-            const unsigned long long slot = atomicAdd(o + 11, 1ull);
-            if (slot < 1000) {
-                unsigned long long* r = o + 16 + 6 * slot;
-                r[0] = now - cp_s;
-                r[1] = coop_on ? now - cp_r0 : 0;
-                r[2] = cp_n[3];
-                r[3] = cp_n[2];
-                r[4] = cp_maxlive;
-                r[5] = cp_s;
-            }
-        }
-    }
-#endif
+    VR_CP_DUMP();
 #undef VR_CP
+#undef VR_CPN
+#undef VR_CP_PHASE_A
+#undef VR_CP_TAIL
+#undef VR_CP_DUMP
 
     if (COUNT) {
         atomicAdd(&A.counters[kCntBoxTests], (unsigned long long)cnt.box_tests);
