@@ -543,6 +543,9 @@ def main():
     ap.add_argument("--drop-in-threads", type=int, default=8)
     ap.add_argument("--no-drop-in", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes of the roofline")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="frames alternate over this many streams / record buffers (2: a frame's render "
+                         "overlaps the previous frame's launch tail, ordered reduce and collective)")
     ap.add_argument("--host-build", action="store_true",
                     help="render the host-built traversal tree instead of the device-built one (same images)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
@@ -602,17 +605,26 @@ def main():
         build["other_build"] = "device-built (VR_SCENE_DEVICE_SAH)" if args.host_build else \
             "host-built (median ranks + binned SAH + 4-wide on the CPU)"
     tile = Tile(0, W, 0, H)
-    state = torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}")
-    stream = torch.cuda.current_stream()
+    # frames alternate over `streams` streams, each with its own record buffer (and, inside the
+    # library, its own call context): frame i+1's render starts while frame i's launch tail, ordered
+    # reduce and cross-GPU collective finish (1: frames strictly one after another)
+    nstreams = max(1, args.streams)
+    states = [torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}") for _ in range(nstreams)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+    state, stream = states[0], streams[0]
 
     def step(i, spp_r, timer=None, timed=False, defer=False):
         # defer: the render's HIP events are recorded but not waited for (VR_LAUNCH_DEFER_TIMES), so
         # back-to-back timed frames queue without a host round trip between them; their times are
         # collected after the timed region
+        j = i % nstreams
+        st_j = streams[j]
+
         def shard(first, st):
-            return render_tile_device(dscene, tile, H, W, spp_r, SEED, first, st.data_ptr(), stream.cuda_stream,
+            return render_tile_device(dscene, tile, H, W, spp_r, SEED, first, st.data_ptr(), st_j.cuda_stream,
                                       timed=timed and not defer, defer_times=defer, device=local)
-        return D.frame_step(shard, state, i, spp_r, timer=timer)
+        with torch.cuda.stream(st_j):  # the collective, the zeroing and the timer events follow the render
+            return D.frame_step(shard, states[j], i, spp_r, timer=timer)
 
     def timed_region(spp_r, first_step):
         """args.warmup untimed + args.steps timed frames of spp_r samples per pixel on every rank,
@@ -633,10 +645,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        stream_check_error(dscene, stream.cuda_stream, device=local)  # device errors of the untimed steps
-        # the timed frames' HIP-event times (render kernel on the launch stream; the ordered per-pixel
-        # Kahan reduce after it), and their device errors
-        lt = collect_launch_times(dscene, stream.cuda_stream, device=local)
+        lt = {"launches": 0, "kernel_ms": 0.0, "reduce_ms": 0.0, "max_passes": 0}
+        for st_j in streams:
+            stream_check_error(dscene, st_j.cuda_stream, device=local)  # device errors of the untimed steps
+            # the timed frames' HIP-event times (render kernel on its launch stream; the ordered
+            # per-pixel Kahan reduce after it), and their device errors
+            lj = collect_launch_times(dscene, st_j.cuda_stream, device=local)
+            for k in ("launches", "kernel_ms", "reduce_ms"):
+                lt[k] += lj[k]
+            lt["max_passes"] = max(lt["max_passes"], lj["max_passes"])
         assert lt["launches"] == args.steps, lt
         if distributed:
             t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -694,7 +711,7 @@ def main():
                 f"{os.path.basename(args.mesh)} (sha256-verified reference bunny), counter-based RNG seed 0x5EED0001",
         "config": {"workload": workload, "config": args.config, "width": W, "height": H, "spp_per_gpu": spp,
                    "triangles": info["triangle_count"], "bvh_depth": info["max_bvh_depth"],
-                   "parallelism": f"spp-split x{world}, RCCL reduce",
+                   "parallelism": f"spp-split x{world}, RCCL reduce", "streams": nstreams,
                    "pmc_key": config_key(cfg["scene"], W, H, spp)},
     }
     # samples of 8x8 blocks whose camera rays all miss every object (block_cull_kernel) are applied

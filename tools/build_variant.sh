@@ -12,7 +12,8 @@ for s in vr_render.hip vr_image.hip vr_build.hip vr_host.cpp; do
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done  # set -e: a failed compile stops the link
-mkdir -p ab
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUT/*.o -lz -o ab/lib$NAME.so
+D=${OUTDIR:-ab}
+mkdir -p $D
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUT/*.o -lz -o $D/lib$NAME.so
 rm -rf "$OUT"
-echo ab/lib$NAME.so
+echo $D/lib$NAME.so

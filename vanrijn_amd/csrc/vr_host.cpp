@@ -999,6 +999,18 @@ int check_render_params(const vr_scene* s, const vr_render_params* p) {
     return VR_OK;
 }
 
+// persistent grid: workgroups per CU of the render kernel (3: 3 waves per SIMD); VR_GRID_PER_CU
+// overrides (tuning builds; diagnostic: throughput against occupancy)
+int grid_per_cu() {
+    const char* g = tuning_env("VR_GRID_PER_CU");
+    return g ? std::max(1, atoi(g)) : 3;
+}
+// ... of the cooperative-tail instantiations (vr_render.hip VR_COOP_MINW waves per SIMD)
+int coop_grid_per_cu() {
+    const char* g = tuning_env("VR_COOP_GRID");
+    return g ? std::max(1, atoi(g)) : 2;
+}
+
 vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* state) {
     vr::RenderArgs a{};
     a.scene = s->dev;
@@ -1057,6 +1069,13 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         const uint64_t waves = (uint64_t)std::max(1, s->cu_count) * 3 * 4;
         const uint64_t g = items / (waves * 80) / 64 * 64;
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
+    }
+    {
+        // guided slices near the end of the queue (RenderArgs::taper_rcp): 1 / (4 x the launch's
+        // persistent waves)
+        const char* tp = tuning_env("VR_TAPER");  // tuning hook: 0 off
+        const double waves = (double)std::max(1, s->cu_count) * grid_per_cu() * 4;
+        a.taper_rcp = (tp && atoi(tp) == 0) || a.grab == 0 ? 0.0 : 1.0 / (4.0 * waves);
     }
     const char* lt = tuning_env("VR_LEAF_THRESHOLD");  // tuning hooks
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
@@ -1723,12 +1742,6 @@ struct DoneOnExit {
     ~DoneOnExit() { (void)hipEventRecord(done, st); }
 };
 
-// persistent grid: workgroups per CU of the render kernel (3: 3 waves per SIMD); VR_GRID_PER_CU
-// overrides (diagnostic: throughput against occupancy)
-int grid_per_cu() {
-    static const int per_cu = tuning_env("VR_GRID_PER_CU") ? std::max(1, atoi(tuning_env("VR_GRID_PER_CU"))) : 3;
-    return per_cu;
-}
 
 int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* state, hipStream_t st, int32_t* err,
                    bool counting, bool recording, void* records, unsigned long long* counters,
@@ -1853,7 +1866,10 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         lc.coop = a.coop != 0 && !recording && !counting && !lc.big && s->dev.integrator != 1 && s->dark0 &&
                   (lc.mats & 2);
         if (variant) *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u);
-        int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * grid_per_cu(), st, mid);
+        // the COOP instantiations run at VR_COOP_MINW (2) waves per SIMD: a third workgroup per CU
+        // could not be resident and would start only as others retire
+        const int per_cu = lc.coop ? coop_grid_per_cu() : grid_per_cu();
+        int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * per_cu, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));
         if (timing) {
             hipEvent_t end = timing->add();
