@@ -543,9 +543,10 @@ def main():
     ap.add_argument("--drop-in-threads", type=int, default=8)
     ap.add_argument("--no-drop-in", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes of the roofline")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=None,
                     help="frames alternate over this many streams / record buffers (2: a frame's render "
-                         "overlaps the previous frame's launch tail, ordered reduce and collective)")
+                         "overlaps the previous frame's launch tail, ordered reduce and collective); "
+                         "default 1 on one GPU, 2 at N > 1")
     ap.add_argument("--host-build", action="store_true",
                     help="render the host-built traversal tree instead of the device-built one (same images)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
@@ -577,7 +578,9 @@ def main():
     # so a one-GPU box rehearses the multi-GPU step (init, barriers, reduce, max-over-ranks timing)
     distributed = world > 1 or "RANK" in os.environ
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # a generous timeout: the other ranks wait in the final barrier while rank 0 runs its PMC passes
+        import datetime
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=datetime.timedelta(minutes=30))
         world = dist.get_world_size()  # what the line reports as n_gpus
         assert world == args.gpus, (world, args.gpus)
 
@@ -608,7 +611,10 @@ def main():
     # frames alternate over `streams` streams, each with its own record buffer (and, inside the
     # library, its own call context): frame i+1's render starts while frame i's launch tail, ordered
     # reduce and cross-GPU collective finish (1: frames strictly one after another)
-    nstreams = max(1, args.streams)
+    # Measured on one MI355X (profiles/r06/probe): 1024^2 @32 spp -- the per-rank frame at N = 8 --
+    # 5.95 -> 5.54 ms per frame with 2 streams; @256 spp (N = 1) 41.18 -> 41.36 ms (no gain): so 2
+    # streams where the ranks' frames are short and a collective follows each one
+    nstreams = max(1, args.streams if args.streams else (2 if world > 1 else 1))
     states = [torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}") for _ in range(nstreams)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     state, stream = states[0], streams[0]

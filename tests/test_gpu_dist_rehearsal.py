@@ -25,17 +25,20 @@ def _free_port():
 
 
 @pytest.mark.gpu
-def test_bench_under_torchrun_world_one():
+@pytest.mark.parametrize("streams", [1, 2])
+def test_bench_under_torchrun_world_one(streams):
+    """streams 2: the N > 1 default (frames alternate over two streams and record buffers, each
+    frame's reduce issued from its own stream); PMC passes of rank 0 on the first run only."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "c2", "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline", "--no-drop-in"]
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "c2", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--no-drop-in", "--streams", str(streams)] + (["--no-pmc"] if streams == 2 else [])
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 1 and out["steps"] == 2
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["config"]["streams"] == streams
     assert out["config"]["parallelism"] == "spp-split x1, RCCL reduce"
     assert out["value"] > 0 and out["ms_per_step"] > 0
     # one frame of C2 is 512 x 512 x 64 samples; value = samples / max-over-ranks time

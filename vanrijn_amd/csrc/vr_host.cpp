@@ -1005,10 +1005,14 @@ int grid_per_cu() {
     const char* g = tuning_env("VR_GRID_PER_CU");
     return g ? std::max(1, atoi(g)) : 3;
 }
-// ... of the cooperative-tail instantiations (vr_render.hip VR_COOP_MINW waves per SIMD)
+// ... of the cooperative-tail instantiations.  They run at VR_COOP_MINW = 2 waves per SIMD, so only 2
+// workgroups per CU are resident; the third starts as another retires.  Kept on purpose:
+// C1 1.558 ms at 3 per CU against 1.572-1.604 at 2 (9 interleaved repetitions each,
+// profiles/r06/probe/coopgrid.out) -- a late-starting workgroup takes items the resident ones would
+// otherwise have taken in their tails
 int coop_grid_per_cu() {
     const char* g = tuning_env("VR_COOP_GRID");
-    return g ? std::max(1, atoi(g)) : 2;
+    return g ? std::max(1, atoi(g)) : 3;
 }
 
 vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* state) {
@@ -1069,13 +1073,6 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         const uint64_t waves = (uint64_t)std::max(1, s->cu_count) * 3 * 4;
         const uint64_t g = items / (waves * 80) / 64 * 64;
         a.grab = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(128, g));
-    }
-    {
-        // guided slices near the end of the queue (RenderArgs::taper_rcp): 1 / (4 x the launch's
-        // persistent waves)
-        const char* tp = tuning_env("VR_TAPER");  // tuning hook: 0 off
-        const double waves = (double)std::max(1, s->cu_count) * grid_per_cu() * 4;
-        a.taper_rcp = (tp && atoi(tp) == 0) || a.grab == 0 ? 0.0 : 1.0 / (4.0 * waves);
     }
     const char* lt = tuning_env("VR_LEAF_THRESHOLD");  // tuning hooks
     a.leaf_threshold = lt ? (uint32_t)std::max(1, atoi(lt)) : 48u;
@@ -1866,8 +1863,7 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         lc.coop = a.coop != 0 && !recording && !counting && !lc.big && s->dev.integrator != 1 && s->dark0 &&
                   (lc.mats & 2);
         if (variant) *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u);
-        // the COOP instantiations run at VR_COOP_MINW (2) waves per SIMD: a third workgroup per CU
-        // could not be resident and would start only as others retire
+        // the COOP instantiations (2 waves per SIMD) keep 3 workgroups per CU (coop_grid_per_cu)
         const int per_cu = lc.coop ? coop_grid_per_cu() : grid_per_cu();
         int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * per_cu, st, mid);
         if (lr) return fail(lr == -1000 ? VR_ERROR_UNSUPPORTED : VR_ERROR_DEVICE, vr::device_error_string(lr));

@@ -169,12 +169,6 @@ struct RenderArgs {
     // work-item decode without integer division: 1 / (8x8 blocks per sample round), 1 / (blocks
     // per row), as f64 (a 32-bit quotient from one f64 product is off by at most one, then fixed)
     double rcp_blocks, rcp_bw;
-    // guided slices (round 6): near the end of the queue a wave's slice shrinks to its share of
-    // what is left -- min(grab, max(64, remaining x taper_rcp)) items, remaining estimated from
-    // where the wave's previous slice ended, taper_rcp = 1 / (4 x waves) -- so the launch's waves
-    // run out of work together instead of some starting a full 512-item slice (8 samples a lane)
-    // as the queue empties; 0: every slice is `grab` items
-    double taper_rcp;
     unsigned long long* queue;    // work-item counter (zeroed before the launch)
     double* staging;              // [pass sample][tile pixel][2] final photon {wavelength, intensity}
     // [tile pixels][4] sums {X, Y, Z, weight}, then [tile pixels][4] compensations {X, Y, Z,

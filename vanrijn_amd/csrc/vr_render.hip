@@ -1164,18 +1164,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 } else {
                     // wave-private slice of the queue: one atomic per `grab` items
                     if (w_next >= w_end) {
-                        // guided slices (RenderArgs::taper_rcp): the wave's share of what is left,
-                        // estimated from its previous slice's end (an overestimate: other waves have
-                        // taken more since), in multiples of 64 items, between 64 and grab
-                        uint32_t want = A.grab;
-                        if (A.taper_rcp != 0.0 && w_end < items) {
-                            const uint32_t g = (uint32_t)fmin((double)(items - w_end) * A.taper_rcp, (double)A.grab);
-                            want = max(64u, g & ~63u);
-                        }
-                        want = __builtin_amdgcn_readfirstlane(want);
-                        if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)want);
+                        if (lane == leader) base = atomicAdd(A.queue, (unsigned long long)A.grab);
                         w_next = uniform64(__shfl(base, (int)leader));
-                        w_end = w_next + want;
+                        w_end = w_next + A.grab;
                     }
                     const uint64_t avail = w_end - w_next;
                     base = w_next;
