@@ -1015,6 +1015,14 @@ int coop_grid_per_cu() {
     return g ? std::max(1, atoi(g)) : 3;
 }
 
+#ifdef VR_SPLIT_PROBE  // analysis builds: the ray dump every render launch appends to (vr_probe_set_dump)
+struct {
+    double* rays;
+    unsigned long long* count;
+    uint64_t cap;
+} g_probe = {nullptr, nullptr, 0};
+#endif
+
 vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* state) {
     vr::RenderArgs a{};
     a.scene = s->dev;
@@ -1025,6 +1033,11 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
     a.width = p->width;
     a.height = p->height;
     a.seed = p->seed;
+#ifdef VR_SPLIT_PROBE
+    a.probe_rays = g_probe.rays;
+    a.probe_count = g_probe.count;
+    a.probe_n = g_probe.cap;
+#endif
     {  // vr-hash32 v2: the launch-constant key of stream_base_keyed
         uint64_t z = p->seed ^ 0x76616E52696A6E31ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -2485,4 +2498,60 @@ int vr_write_png(const char* path, const uint8_t* rgb, uint32_t width, uint32_t 
     return VR_OK;
 }
 
+#ifdef VR_SPLIT_PROBE
+// Analysis builds only (-DVR_SPLIT_PROBE; tools/split_probe.py, DESIGN.md section 6 "the megakernel
+// split").  vr_probe_set_dump: every later render launch appends each ray it traces (origin,
+// direction: 6 f64) to the device buffer `rays` (at most `cap`; *count, a device counter, takes the
+// number of rays met); null turns the dump off.  vr_probe_trace: the traversal-only TRACE
+// instantiation of the render kernel over n device rays, closest hits (distance; object << 32 |
+// index << 2 | kind) into `hits`, at `minw` waves per SIMD and `per_cu` workgroups per CU, 16-bit
+// stack entries when s16; *ms: the kernel's HIP-event time.
+int vr_probe_set_dump(double* rays, unsigned long long* count, uint64_t cap) {
+    g_probe.rays = rays;
+    g_probe.count = count;
+    g_probe.cap = rays ? cap : 0;
+    return VR_OK;
+}
+
+int vr_probe_trace(const vr_scene* s, const double* rays, uint64_t n, double* hits, int minw, int s16, int per_cu,
+                   void* stream, float* ms) {
+    if (!s || !rays || !hits) return fail(VR_ERROR_INVALID_ARGUMENT, "null argument");
+    if (s16 && s->wide_count >= 65536) return fail(VR_ERROR_UNSUPPORTED, "16-bit stack entries need < 65536 wide nodes");
+    VR_HIP(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    static unsigned long long* q = nullptr;
+    static int32_t* err = nullptr;
+    if (!q) VR_HIP(hipMalloc(&q, 256));
+    if (!err) VR_HIP(hipMalloc(&err, 256));
+    vr_render_params p{};
+    p.tile.end_column = 1;
+    p.tile.end_row = 1;
+    p.width = p.height = 1;
+    p.spp = 1;
+    vr::RenderArgs a = make_args(s, &p, nullptr);
+    a.probe_rays = rays;
+    a.probe_hits = hits;
+    a.probe_n = n;
+    a.probe_count = nullptr;
+    a.grab = 512;
+    a.queue = q;
+    a.error_flag = err;
+    VR_HIP(hipMemsetAsync(q, 0, 256, st));
+    VR_HIP(hipMemsetAsync(err, 0, 256, st));
+    hipEvent_t e0, e1;
+    VR_HIP(hipEventCreate(&e0));
+    VR_HIP(hipEventCreate(&e1));
+    VR_HIP(hipEventRecord(e0, st));
+    const int lr = vr::launch_trace_probe(a, wide_stack_depth(s), minw, s16 != 0, std::max(1, s->cu_count) * per_cu, st);
+    VR_HIP(hipEventRecord(e1, st));
+    VR_HIP(hipEventSynchronize(e1));
+    float t = 0.f;
+    VR_HIP(hipEventElapsedTime(&t, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (lr) return fail(VR_ERROR_UNSUPPORTED, "no TRACE instantiation for this stack / waves choice");
+    if (ms) *ms = t;
+    return VR_OK;
+}
+#endif
 }  // extern "C"

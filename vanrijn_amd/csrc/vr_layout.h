@@ -188,6 +188,14 @@ struct RenderArgs {
     const uint32_t* live_count;
     // debug builds only (-DVR_STAGE_GUARD, DESIGN.md section 8 "staging invariant"): beside every
     // staged photon the launch's generation, which the ordered reduce checks before reading it
+    // analysis builds only (-DVR_SPLIT_PROBE, DESIGN.md section 6 "the megakernel split"): the render
+    // kernel appends every traced ray (6 f64) to probe_rays (probe_count: the next slot; at most
+    // probe_n); the TRACE kernel reads probe_n rays from it and writes their closest hits (2 f64
+    // each) to probe_hits
+    const double* probe_rays;
+    double* probe_hits;
+    unsigned long long* probe_count;
+    uint64_t probe_n;
     uint32_t* stage_tag;  // [pass sample][tile pixel], or nullptr
     uint32_t stage_gen;   // this pass's generation (never 0)
     uint32_t pad_gen;
@@ -260,6 +268,9 @@ int device_build_sah(TriVerts* tris, TriNormals* normals, uint32_t n, int32_t no
 // vr_build.hip: Node4 / Node4x records from a device-built binary tree and a host-made descriptor
 int device_fill_wide(const Node* bin, const int32_t* desc, uint64_t n4, Node4* out4, void* stream);
 int launch_trace(const TraceArgs& args, int stack_depth, void* stream);
+#ifdef VR_SPLIT_PROBE  // analysis builds (vr_render.hip)
+int launch_trace_probe(const RenderArgs& args, int stack_depth, int minw, bool s16, int grid, void* stream);
+#endif
 const char* device_error_string(int code);
 
 }  // namespace vr

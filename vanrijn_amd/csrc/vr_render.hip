@@ -27,6 +27,7 @@
 #include <float.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 
 #include "../../include/vanrijn_amd.h"
 #include "rgb_spectrum_tables.h"
@@ -175,15 +176,22 @@ __device__ void coop_prof_dump(unsigned long long* o, bool coop_on, unsigned lan
 // BIG: 64-bit byte offsets for the node and triangle loads -- scenes whose triangle array reaches 4 GB
 // (53.7 M triangles) or whose 4-wide tree has 2^25 nodes (vr_host.cpp needs_big_offsets); every other
 // scene's kernels address both arrays with 32-bit offsets from the scalar base (the loads' saddr form)
+// TRACE (analysis builds, -DVR_SPLIT_PROBE: DESIGN.md section 6, "the megakernel split"): the same
+// kernel as a traversal-only pass over a buffer of rays -- work items are rays (RenderArgs::probe_rays,
+// 6 f64 each), phase A stores each closest hit (probe_hits, 2 f64: distance, kind | index << 2 and
+// object) instead of shading, and no path state exists, so the register peak is traversal's alone.
+// S16: 16-bit LDS stack entries (trees below 65,536 wide nodes): half the stack's LDS, so more
+// workgroups fit a CU.
 template <int STACK, bool COUNT, bool RECORD, bool DARK0, int MATS = 3, int MINW = 3, bool WHITTED = false,
-          bool COOP = false, bool BIG = false>
+          bool COOP = false, bool BIG = false, bool TRACE = false, bool S16 = false>
 // The scene's small uniform tables (planes / spheres, materials, BVH roots) come in again as
 // restrict-qualified arguments: nothing the kernel stores can alias them, so their wave-uniform
 // reads compile to scalar loads (the scalar cache) instead of vector loads through L2.
 __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const Prim* __restrict__ g_prims,
                                                            const Material* __restrict__ g_materials,
                                                            const Bvh* __restrict__ g_bvhs) {
-    __shared__ uint32_t st_node[STACK * 256];
+    typedef typename std::conditional<S16, uint16_t, uint32_t>::type StackT;
+    __shared__ StackT st_node[STACK * 256];
     // leaf triangles met during traversal wait for a leaf round, in which every lane tests one: the
     // f64 triangle test then runs for many lanes at once instead of for the few that reached a leaf
     // in this step.  Per wave: the FIFO of queued leaves (triangle | exact-box flag, and the owning
@@ -478,6 +486,20 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // there, not in registers of its own that would stay live through the traversal phase):
     // primitive lists first, then the BVHs
     auto begin_ray = [&]() {
+#ifdef VR_SPLIT_PROBE  // analysis builds: every traced ray's (origin, direction) into probe_rays
+        if (!TRACE && A.probe_rays) {
+            const uint64_t m = exec_mask();
+            const unsigned leader = (unsigned)__builtin_ctzll(m);
+            unsigned long long b = 0;
+            if (lane == leader) b = atomicAdd(A.probe_count, (unsigned long long)__popcll(m));
+            const uint64_t slot = uniform64(__shfl(b, (int)leader)) + lanes_below(m);
+            if (slot < A.probe_n) {
+                double* r = const_cast<double*>(A.probe_rays) + 6 * slot;
+                r[0] = pre.o.x; r[1] = pre.o.y; r[2] = pre.o.z;
+                r[3] = pre.d.x; r[4] = pre.d.y; r[5] = pre.d.z;
+            }
+        }
+#endif
         pre = prepare(Ray{pre.o, pre.d});
         pre32 = prepare32(pre, S.extent);
         if (COUNT) cnt.rays++;
@@ -935,7 +957,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         uint32_t brank = (uint32_t)pi((int)best.rank);
         double bd = p64(best.d);
         // frontier entry f of this half: row f / hs, column hb + f % hs of the wave's stack words
-        auto fr = [&](int f) -> uint32_t& {
+        auto fr = [&](int f) -> StackT& {
             return st_node[(f >> hshift) * 256 + (tid & ~63) + hb + (f & (hs - 1))];
         };
         const int cap = hs * STACK;
@@ -1085,7 +1107,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
             // lanes still traverse: the deferred lanes wait (state kTraversed) and the next phase
             // A shades them with more lanes busy (misses are finished at once either way)
             bool shade_now = true, finish_now = true;
-            if (A.shade_min | A.miss_min) {
+            if constexpr (TRACE) {
+                if (state == kTraversed) {  // the ray's closest hit, then the next ray
+                    double* h = A.probe_hits + 2 * (uint64_t)px;
+                    __builtin_nontemporal_store(best.d, &h[0]);
+                    __builtin_nontemporal_store(__longlong_as_double(
+                        (long long)(((uint64_t)(uint32_t)best.object << 32) | ((uint32_t)best.index << 2) | (uint32_t)best.kind)), &h[1]);
+                    ++s_idx;
+                    state = kNeedRay;
+                }
+            } else if (A.shade_min | A.miss_min) {
                 const bool idle = lanes_ieq(state, kTraversing) == 0;
                 const uint64_t done_trav = lanes_ieq(state, kTraversed);
                 const int nhit = __popcll(done_trav & lanes_ine((int)best.kind, (int)kNone));
@@ -1093,7 +1124,7 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 shade_now = nhit >= (int)A.shade_min || idle;
                 finish_now = nmiss >= (int)A.miss_min || idle;
             }
-            if (state == kTraversed && (best.kind == kNone ? finish_now : shade_now)) {
+            if (!TRACE && state == kTraversed && (best.kind == kNone ? finish_now : shade_now)) {
                 VR_MARK("traversed");
                 // one call site for shade(): two inlined copies would both run whenever a wave
                 // holds camera-ray hits and bounce hits at once
@@ -1174,7 +1205,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                     const uint64_t want = (uint64_t)__popcll(m);
                     w_next = uniform64(w_next + (want < avail ? want : avail));
                 }
-                if (take) {
+                if (TRACE && take) {  // a work item is one ray of probe_rays
+                    const uint64_t g = base + rank;
+                    if (g >= A.probe_n) {
+                        state = kDone;
+                    } else {
+                        px = (uint32_t)g;
+                        s_idx = 0;
+                        s_end = 1;
+                    }
+                } else if (take) {
                     const uint64_t g = base + rank;
                     if (g >= items) {
                         state = kDone;
@@ -1225,7 +1265,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
             }
             VR_STAMP(1);
-            if (state == kNeedRay) {
+            if (TRACE && state == kNeedRay) {
+                const double* r = A.probe_rays + 6 * (uint64_t)px;
+                pre.o = mk(__builtin_nontemporal_load(&r[0]), __builtin_nontemporal_load(&r[1]),
+                           __builtin_nontemporal_load(&r[2]));
+                pre.d = mk(__builtin_nontemporal_load(&r[3]), __builtin_nontemporal_load(&r[4]),
+                           __builtin_nontemporal_load(&r[5]));
+                state = kRayReady;
+            } else if (state == kNeedRay) {
                 const uint64_t row = A.start_row + py, col = A.start_column + px;
                 rng.reset(stream_base_keyed(A.seed_key, row * A.width + col, A.first_sample + s_idx));
                 // ImageSampler (camera.rs:24-66): film (w/h, 1) or (1, w/h); x's draw first
@@ -1932,6 +1979,32 @@ int launch_trace(const TraceArgs& a, int stack_depth, void* stream) {
     else return -1000;
     return (int)hipGetLastError();
 }
+
+#ifdef VR_SPLIT_PROBE
+// analysis builds: the traversal-only instantiations (TRACE) of the render kernel over a ray buffer,
+// at `minw` waves per SIMD, with 32- or 16-bit LDS stack entries
+int launch_trace_probe(const RenderArgs& a, int stack_depth, int minw, bool s16, int grid, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    dim3 g((unsigned)grid), b(256);
+#define VR_KT(ST, MW, S16_)                                                                                    \
+    hipLaunchKernelGGL((dev::render_kernel<ST, false, false, true, 3, MW, false, false, false, true, S16_>), g, b, \
+                       0, s, a, a.scene.prims, a.scene.materials, a.scene.bvhs)
+    if (stack_depth > 32) return -1000;
+    if (s16) {
+        if (minw == 3) VR_KT(32, 3, true);
+        else if (minw == 4) VR_KT(32, 4, true);
+        else if (minw == 5) VR_KT(32, 5, true);
+        else if (minw == 6) VR_KT(32, 6, true);
+        else return -1001;
+    } else {
+        if (minw == 3) VR_KT(32, 3, false);
+        else if (minw == 4) VR_KT(32, 4, false);
+        else return -1001;
+    }
+#undef VR_KT
+    return (int)hipGetLastError();
+}
+#endif
 
 const char* device_error_string(int code) {
     if (code == -1000) return "BVH deeper than the largest traversal stack (48)";
