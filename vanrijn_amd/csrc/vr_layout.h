@@ -145,8 +145,9 @@ struct RenderArgs {
     uint32_t leaf_threshold;      // leaf round once this many lanes have a pending triangle ...
     uint32_t leaf_stall;          // ... or this many lanes cannot step without one
     uint32_t leaf_few;            // ... or at most this many lanes are still traversing
-    // the launch's tail (COOP instantiations): a wave's last 1 or 2 paths walk their trees with the
-    // wave's lanes once each has bounced `coop_bounces` times; coop = owners served (0: off)
+    // the launch's tail (COOP instantiations): a wave's last 1 to `coop` (4) paths walk their trees
+    // with the wave's lanes once each has bounced `coop_bounces` times (coop_step: 1 or 2 owners,
+    // lone_walk's whole walks: up to 4); 0: off
     uint32_t coop;
     uint32_t coop_bounces;
     // 1: the tail's walks with nothing pending run whole in lone_walk (0: coop_step only; test hook)

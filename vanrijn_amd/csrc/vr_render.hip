@@ -914,11 +914,13 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         q_tail = __builtin_amdgcn_readfirstlane(q_tail);
     };
     // The cooperative tail's walks with nothing pending (no stack entries, no queued leaves, an empty
-    // wave FIFO) for the one or two traversing paths `own` of a wave whose other lanes are done: the
+    // wave FIFO) for the one to four traversing paths `own` of a wave whose other lanes are done: the
     // whole rest of each path's walk of its current BVH in one call.  With one owner every lane
     // works for it; with two the lower half works for the lower owner and the upper half for the
-    // other, both walks at once.  An owner's frontier of nodes to visit is a LIFO over its half's
-    // columns of the wave's stack words; each iteration pops up to one node per four workers, each
+    // other, with three or four each quarter of the wave for one of them (round 6: C1 frames whose
+    // waves kept three trapped mirror paths took 3.9-5.3 ms against ~1.55 ms, profiles/r06/split/
+    // c1_frames.json), all walks at once.  An owner's frontier of nodes to visit is a LIFO over its
+    // group's columns of the wave's stack words; each iteration pops up to one node per four workers, each
     // worker tests one child box against the owner's ray, the hit interior children are pushed and
     // the hit leaves tested at once, one per worker.  The round's candidate (minimum distance, then the
     // highest reference rank) is merged with takes_hit's rule, as in leaf_round, so each path gets
@@ -926,15 +928,20 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
     // per-step owner-state permutes and stack remapping and the separate leaf rounds through the FIFO
     // (C1: the trapped mirror paths' last bounces).  Called with the whole wave active.
     auto lone_walk = [&](const uint64_t own) {
-        const int oa = (int)__builtin_ctzll(own), ob = (int)(63 - __builtin_clzll(own));
-        const bool two = oa != ob;  // wave-uniform
-        const bool upper = two && lane >= 32;
-        const int hb = upper ? 32 : 0, hshift = two ? 5 : 6, hs = 1 << hshift;
+        // 1, 2 or up to 4 owners (wave-uniform): the whole wave, its halves or its quarters work for
+        // them, group g for the g-th lowest owner lane (with 3 owners the last quarter idles)
+        const int nown = __popcll(own);
+        const int hshift = nown == 1 ? 6 : (nown == 2 ? 5 : 4), hs = 1 << hshift;
+        const int grp = (int)lane >> hshift;
+        const int hb = grp << hshift;
         const int r = (int)lane - hb;  // worker rank
-        const uint64_t gmask = two ? (upper ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) : ~0ull;
-        // this half's owner's ray, cull bounds and closest hit, by cross-lane permute (per-lane copies:
-        // uniform copies of both owners' values would need ~80 SGPRs, spilled)
-        const int ow = upper ? ob : oa;
+        const uint64_t gmask = hs == 64 ? ~0ull : (((1ull << hs) - 1) << hb);
+        // this group's owner's ray, cull bounds and closest hit, by cross-lane permute (per-lane
+        // copies: uniform copies of the owners' values would need ~40 SGPRs per owner, spilled)
+        const uint64_t own1 = own & (own - 1), own2 = own1 & (own1 - 1), own3 = own2 & (own2 - 1);
+        const uint64_t mine_o = grp == 0 ? own : (grp == 1 ? own1 : (grp == 2 ? own2 : own3));
+        const bool has_owner = mine_o != 0;
+        const int ow = has_owner ? (int)__builtin_ctzll(mine_o) : (int)lane;
         auto p64 = [&](double v) { return __shfl(v, ow); };
         auto p32 = [&](float v) { return __shfl(v, ow); };
         auto pi = [&](int v) { return __shfl(v, ow); };
@@ -965,14 +972,14 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
         // entry per iteration is a depth-first walk of one subtree, which needs at most the per-lane
         // walk's stack (< STACK) plus one word per level (it pushes every hit child), < 2 * STACK
         const int safe = cap - 4 * STACK;
-        int32_t* const leaves = &wl_tri[wbase + (upper ? kWaveList / 2 : 0)];  // <= 4 per worker
-        static_assert(kWaveList / 2 >= 4 * 64, "each half of the wave FIFO holds a step's leaves");
+        int32_t* const leaves = &wl_tri[wbase + grp * (hs * kPend)];  // <= 1 per worker per step
+        static_assert(kPend >= 1, "each group's share of the wave FIFO holds a step's leaves");
         // the owner's current node, permuted with the whole wave active: ds_bpermute reads 0 from a
         // source lane outside exec, so a permute inside `r == 0` (lanes 0 / 32 only) would start
         // the walk at node 0 whenever the owner is another lane
         const int start = pi(node);
         if (r == 0) fr(0) = (uint32_t)start;
-        int n = 1;  // this half's frontier size
+        int n = has_owner ? 1 : 0;  // this group's frontier size
         while (true) {
             const bool act = n > 0;
             if (__ballot(act) == 0) break;
@@ -1076,8 +1083,9 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 }
             }
         }
-        // each owner takes its half's results (from the half's first lane)
-        const int src = (two && (int)lane == ob) ? 32 : 0;
+        // each owner takes its group's results (from the group's first lane: the owners below it
+        // count its group)
+        const int src = (int)lanes_below(own) << hshift;
         const double rd = __shfl(bd, src);
         const int rkind = __shfl(bkind, src), rindex = __shfl(bindex, src), robject = __shfl(bobject, src);
         const uint32_t rrank = (uint32_t)__shfl((int)brank, src);
@@ -1343,12 +1351,16 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                         // the traversing paths' walks of their BVHs at once when nothing is pending
                         const uint64_t busy = lanes_ieq(state, kTraversing);
                         const uint64_t fresh = busy & lanes_ige(node, 0) & lanes_ieq(sp, 0) & lanes_ieq(np, 0);
-                        if (A.lone_walk && busy != 0 && fresh == busy && __popcll(busy) <= 2 && q_head == q_tail) {
+                        if (A.lone_walk && busy != 0 && fresh == busy && __popcll(busy) <= 4 && q_head == q_tail) {
                             VR_CPN(3, true);
                             lone_walk(busy);
-                        }
-                        else
+                        } else if (nlive <= 2) {
                             coop_step(live);
+                        } else {
+                            // 3 or 4 live paths with pending work: per-lane steps until every one of
+                            // them is fresh again (each bounce's start), then their whole walks at once
+                            coop = false;
+                        }
                     }
                     VR_CP(1);
                 }
