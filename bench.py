@@ -611,19 +611,23 @@ def main():
     # frames alternate over `streams` streams, each with its own record buffer (and, inside the
     # library, its own call context): frame i+1's render starts while frame i's launch tail, ordered
     # reduce and cross-GPU collective finish (1: frames strictly one after another)
-    # Measured on one MI355X (profiles/r06/probe): 1024^2 @32 spp -- the per-rank frame at N = 8 --
-    # 5.95 -> 5.54 ms per frame with 2 streams; @256 spp (N = 1) 41.18 -> 41.36 ms (no gain): so 2
-    # streams where the ranks' frames are short and a collective follows each one
-    nstreams = max(1, args.streams if args.streams else (2 if world > 1 else 1))
+    # Measured on one MI355X (profiles/r06/probe, r06/small): 1024^2 @32 spp -- the per-rank frame at
+    # N = 8 -- 5.95 -> 5.54 ms per frame with 2 streams, C2 (512^2 @64) 3.32 -> 2.88 ms, C1 (256^2 @16,
+    # a few trapped mirror paths set a frame's time) 1.64 -> 0.86 ms; @256 spp (c3 at N = 1) 41.18 ->
+    # 41.36 ms (no gain): so 2 streams where the ranks' frames are short (<= 64 M samples) or a
+    # collective follows each one.  A line with 2 streams also times the frames strictly one after
+    # another (`sequential`), so each frame's own latency is reported beside the throughput.
+    short = W * H * spp <= (64 << 20)
+    nstreams = max(1, args.streams if args.streams else (2 if world > 1 or short else 1))
     states = [torch.zeros(H * W * 8, dtype=torch.float64, device=f"cuda:{local}") for _ in range(nstreams)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     state, stream = states[0], streams[0]
 
-    def step(i, spp_r, timer=None, timed=False, defer=False):
+    def step(i, spp_r, timer=None, timed=False, defer=False, ns=None):
         # defer: the render's HIP events are recorded but not waited for (VR_LAUNCH_DEFER_TIMES), so
         # back-to-back timed frames queue without a host round trip between them; their times are
         # collected after the timed region
-        j = i % nstreams
+        j = i % (ns or nstreams)
         st_j = streams[j]
 
         def shard(first, st):
@@ -632,12 +636,12 @@ def main():
         with torch.cuda.stream(st_j):  # the collective, the zeroing and the timer events follow the render
             return D.frame_step(shard, states[j], i, spp_r, timer=timer)
 
-    def timed_region(spp_r, first_step):
+    def timed_region(spp_r, first_step, ns=None):
         """args.warmup untimed + args.steps timed frames of spp_r samples per pixel on every rank,
         bracketed by barrier + synchronize; the max over ranks of the wall time, and this rank's
         HIP-event kernel times."""
         for i in range(args.warmup):
-            step(first_step + i, spp_r)
+            step(first_step + i, spp_r, ns=ns)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
@@ -645,7 +649,7 @@ def main():
         events = []
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(first_step + args.warmup + i, spp_r, timer=events, defer=True)
+            step(first_step + args.warmup + i, spp_r, timer=events, defer=True, ns=ns)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
@@ -693,6 +697,16 @@ def main():
                 "spp_per_gpu": cfg["spp"], "render_kernel_ms": round(wr["kernel_s"] * 1e3, 3),
                 "scaling": "weak"}
         progress(f"weak: {weak['ms_per_step']} ms/step")
+    sequential = None
+    if nstreams > 1:
+        # the same frames strictly one after another (one stream): each frame's own latency
+        sr = timed_region(spp, 1 + 4 * (args.warmup + args.steps), ns=1)
+        sequential = {"value": round(samples / sr["elapsed"] / 1e6, 3), "unit": "Msamples/s", "streams": 1,
+                      "ms_per_step": round(sr["elapsed"] / args.steps * 1e3, 3),
+                      "render_kernel_ms": round(sr["kernel_s"] * 1e3, 3)}
+        progress(f"sequential: {sequential['ms_per_step']} ms/step")
+        # the roofline's kernel time from launches that do not overlap another frame's
+        avg_kernel_s = sr["kernel_s"]
     workload = {"main": f"main.rs scene (plane, 3 spheres, Lambertian bunny), {W}x{H}",
                 "bench": f"bench scene (reflective bunny), {W}x{H}",
                 "c5": f"C5: main.rs plane + spheres + 1,051,392-triangle synthetic mesh, {W}x{H}"}[cfg["scene"]]
@@ -726,6 +740,8 @@ def main():
     out["traced_msamples_per_s"] = round(world * args.steps * counts["samples"] / elapsed / 1e6, 3)
     if weak:
         out["weak_scaling"] = weak
+    if sequential:
+        out["sequential"] = sequential
     pmc = None
     if rank == 0 and not args.no_pmc:
         # this rank's shard (at N > 1 too: the PMC child is a one-process run of the same spp)

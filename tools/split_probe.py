@@ -67,6 +67,41 @@ def main():
                                     3 if minw == 3 else (4 if minw == 4 else 5), C.c_void_p(stream), C.byref(ms))
             N.check(rc)
             res.setdefault((minw, s16), []).append(ms.value)
+    if os.environ.get("SPLIT_SORT") == "1":
+        # the same rays reordered by (direction octant, 30-bit Morton code of the origin
+        # in the origins' bounding box) -- the order a split design's ray queue could be sorted into
+        # -- traced again at 3 waves per SIMD; the sort itself timed with CUDA events
+        def spread(x):  # 10 bits -> every third bit
+            x = (x | (x << 16)) & 0x030000FF
+            x = (x | (x << 8)) & 0x0300F00F
+            x = (x | (x << 4)) & 0x030C30C3
+            return (x | (x << 2)) & 0x09249249
+        r6 = rays[:n * 6].view(n, 6)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        o = r6[:, :3]
+        lo, hi = o.min(0).values, o.max(0).values
+        q = ((o - lo) / (hi - lo).clamp_min(1e-300) * 1023.0).clamp(0, 1023).to(torch.int64)
+        key = spread(q[:, 0]) | (spread(q[:, 1]) << 1) | (spread(q[:, 2]) << 2)
+        key |= ((r6[:, 3] < 0).to(torch.int64) << 32) | ((r6[:, 4] < 0).to(torch.int64) << 31) | \
+            ((r6[:, 5] < 0).to(torch.int64) << 30)
+        order = torch.argsort(key)
+        del key, q, o
+        sorted_rays = r6[order].contiguous().view(-1)
+        e1.record()
+        torch.cuda.synchronize()
+        sort_ms = e0.elapsed_time(e1)
+        del order
+        sres = []
+        for rep in range(3):
+            N.check(lib.vr_probe_trace(ds.handle, C.c_void_p(sorted_rays.data_ptr()), n, C.c_void_p(hits.data_ptr()), 3, 0,
+                                       3, C.c_void_p(stream), C.byref(ms)))
+            sres.append(ms.value)
+        print(json.dumps({"scene": which, "size": size, "spp": spp, "rays": n, "order": "octant + origin Morton",
+                          "waves_per_simd": 3, "stack16": 0, "trace_ms_median": round(statistics.median(sres), 3),
+                          "all_ms": [round(x, 3) for x in sres], "sort_ms": round(sort_ms, 3),
+                          "grays_per_s": round(n / statistics.median(sres) / 1e6, 3)}), flush=True)
+        rays = sorted_rays  # the check below then samples the sorted rays and their hits
     # correctness: a strided sample against the exact binary-tree trace kernel
     idx = np.linspace(0, n - 1, min(n, 200000)).astype(np.int64)
     rv = rays.view(-1, 6)[torch.from_numpy(idx).cuda()].cpu().numpy()
