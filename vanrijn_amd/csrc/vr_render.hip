@@ -1905,7 +1905,8 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
     int mats = (c.mats == 1 || c.mats == 2) ? c.mats : 3;
     if (!c.dark0) mats = 3;  // the general kernel
 #ifdef VR_TUNING_VARIANTS  // experiment hooks of tuning builds only (tools/variants.py)
-    // 1..4 = force that many waves per SIMD (default 3); VR_FORCE_MATS: the material specialisation
+    // 1..4 = force that many waves per SIMD (default 3); 5 / 6: 16-bit LDS stack entries (trees below
+    // 65,536 wide nodes only) at 4 / 3 waves per SIMD; VR_FORCE_MATS: the material specialisation
     const char* ve = getenv("VR_KERNEL_VARIANT");
     const int variant = ve ? atoi(ve) : 0;
     if (const char* fm = getenv("VR_FORCE_MATS")) mats = atoi(fm);
@@ -1915,6 +1916,8 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
     else if (variant == 1) VR_K(STACK, false, false, D, M, 1);  \
     else if (variant == 2) VR_K(STACK, false, false, D, M, 2);  \
     else if (variant == 4) VR_K(STACK, false, false, D, M, 4);  \
+    else if (variant == 5 && STACK == 32) VR_K(STACK, false, false, D, M, 4, false, false, false, false, true); \
+    else if (variant == 6 && STACK == 32) VR_K(STACK, false, false, D, M, 3, false, false, false, false, true); \
     else VR_K(STACK, false, false, D, M, 3)
 #else
 #define VR_MODES(D, M)                                    \
