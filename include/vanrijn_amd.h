@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 9
+#define VR_ABI_VERSION 10
 #define VR_MAX_SPECTRUM_SAMPLES 64
 #define VR_RECURSION_LIMIT 128 /* camera.rs:69 */
 
@@ -281,6 +281,7 @@ typedef struct vr_launch_stats {
 } vr_launch_stats;
 #define VR_VARIANT_COOP 1u         /* the cooperative-tail instantiation (small launches, mirror scenes) */
 #define VR_VARIANT_WIDE_OFFSETS 2u /* the 64-bit-offset kernels (VR_SCENE_WIDE_OFFSETS) */
+#define VR_VARIANT_STACK16 4u      /* 16-bit traversal-stack entries (trees below 65,536 wide nodes; ABI 10) */
 
 #define VR_LAUNCH_TIMED 1u    /* bracket the kernel with HIP events and synchronise at the end */
 #define VR_LAUNCH_COUNTERS 2u /* counting build of the kernel (slower), fills the counters */
@@ -302,6 +303,9 @@ typedef struct vr_launch_stats {
 /* cooperative tail without its whole-walk form (the one or two live paths' walks run in coop_step's
  * per-step form only): the same records bit for bit; for tests and A/B measurements (ABI 9) */
 #define VR_LAUNCH_NO_LONE_WALK 64u
+/* keep 32-bit traversal-stack entries where the tree would allow 16-bit ones: the same records bit for
+ * bit; for tests and A/B measurements (ABI 10) */
+#define VR_LAUNCH_STACK32 128u
 
 int vr_render_tile_device(const vr_scene* scene, const vr_render_params* params, double* state, void* stream,
                           uint32_t launch_flags, vr_launch_stats* stats);

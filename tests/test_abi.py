@@ -42,7 +42,7 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_error_strings():
     lib = N.lib()
-    assert lib.vr_abi_version() == 9
+    assert lib.vr_abi_version() == 10
     assert isinstance(lib.vr_last_error(), bytes)
 
 

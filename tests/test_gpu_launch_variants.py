@@ -188,3 +188,34 @@ def test_wide_offset_kernels_are_bit_identical(which):
         out.append((st.cpu(), rec, c["node_visits"]))
     assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))  # bitwise, NaN included
     assert out[0][1].tobytes() == out[1][1].tobytes()
+
+
+@pytest.mark.parametrize("which", ["main", "bench_nocoop"])
+def test_stack16_kernels_are_bit_identical(which):
+    """16-bit traversal-stack entries (trees below 65,536 wide nodes: the bunny's 27 K) against the
+    32-bit ones (VR_LAUNCH_STACK32), fresh and accumulating; the launch reports which ran."""
+    scene = scenes.main_scene() if which == "main" else scenes.bench_scene()
+    ds = scene.device_scene(0, device_sah=True)
+    H, W = 200, 240
+    t = Tile(16, 216, 20, 180)
+    npix = t.width() * t.height()
+    out = []
+    for s16 in (True, False):
+        st = torch.zeros(npix * 8, dtype=torch.float64, device="cuda")
+        # the bench scene's small launches take the cooperative tail (32-bit stacks): without it
+        a = render_tile_device(ds, t, H, W, 12, 0x5EED0001, 0, st.data_ptr(), coop=False, stack16=s16)
+        b = render_tile_device(ds, t, H, W, 5, 0x5EED0001, 12, st.data_ptr(), accumulate=True, coop=False,
+                               stack16=s16)
+        torch.cuda.synchronize()
+        assert bool(a["variant"] & N.VARIANT_STACK16) == s16 and bool(b["variant"] & N.VARIANT_STACK16) == s16
+        out.append(st.cpu())
+    assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
+
+
+def test_stack16_needs_a_small_tree():
+    """C5's 1.05 M-triangle mesh has ~413 K wide nodes: its kernels keep 32-bit stack entries."""
+    ds = scenes.synthetic_scene().device_scene(0, device_sah=True)
+    st = torch.zeros(64 * 64 * 8, dtype=torch.float64, device="cuda")
+    s = render_tile_device(ds, Tile(0, 64, 0, 64), 64, 64, 1, 0x5EED0001, 0, st.data_ptr())
+    torch.cuda.synchronize()
+    assert not s["variant"] & N.VARIANT_STACK16

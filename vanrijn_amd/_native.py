@@ -26,8 +26,8 @@ SCENE_DEVICE_SAH = 8
 SCENE_GREEDY_COLLAPSE = 16
 SCENE_WIDE_OFFSETS = 32
 LAUNCH_TIMED, LAUNCH_COUNTERS, LAUNCH_DEFER_TIMES, LAUNCH_NO_CULL = 1, 2, 4, 8
-LAUNCH_NO_DIST_CULL, LAUNCH_NO_COOP, LAUNCH_NO_LONE_WALK = 16, 32, 64
-VARIANT_COOP, VARIANT_WIDE_OFFSETS = 1, 2
+LAUNCH_NO_DIST_CULL, LAUNCH_NO_COOP, LAUNCH_NO_LONE_WALK, LAUNCH_STACK32 = 16, 32, 64, 128
+VARIANT_COOP, VARIANT_WIDE_OFFSETS, VARIANT_STACK16 = 1, 2, 4
 SCENE_INFO_NAN_FREE = 1
 
 

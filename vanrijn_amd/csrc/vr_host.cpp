@@ -1695,9 +1695,11 @@ int vr_debug_set_fault_object(vr_scene* s, int32_t object) {
 
 int vr_debug_set_launch_flags(vr_scene* s, uint32_t flags) {
     if (!s) return fail(VR_ERROR_INVALID_ARGUMENT, "null scene");
-    const uint32_t allowed = VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP | VR_LAUNCH_NO_LONE_WALK;
+    const uint32_t allowed =
+        VR_LAUNCH_NO_CULL | VR_LAUNCH_NO_DIST_CULL | VR_LAUNCH_NO_COOP | VR_LAUNCH_NO_LONE_WALK | VR_LAUNCH_STACK32;
     if (flags & ~allowed)
-        return fail(VR_ERROR_INVALID_ARGUMENT, "only NO_CULL / NO_DIST_CULL / NO_COOP / NO_LONE_WALK apply to every call");
+        return fail(VR_ERROR_INVALID_ARGUMENT,
+                    "only NO_CULL / NO_DIST_CULL / NO_COOP / NO_LONE_WALK / STACK32 apply to every call");
     s->debug_launch_flags = flags;
     return VR_OK;
 }
@@ -1877,7 +1879,13 @@ int enqueue_passes(vr_scene* s, CallCtx* c, const vr_render_params* p, double* s
         // the cooperative tail's instantiations exist for DARK0 scenes with a reflective material
         lc.coop = a.coop != 0 && !recording && !counting && !lc.big && s->dev.integrator != 1 && s->dark0 &&
                   (lc.mats & 2);
-        if (variant) *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u);
+        // 16-bit LDS stack entries: every node index of the tree fits (round 6, vr_render.hip
+        // launch_render_t; VR_LAUNCH_STACK32 keeps 32-bit entries, the same records bit for bit)
+        lc.s16 = !recording && !counting && !lc.big && !lc.coop && s->dev.integrator != 1 && s->wide_count < 65536 &&
+                 stack <= 32 && !(launch_flags & VR_LAUNCH_STACK32);
+        if (variant)
+            *variant = (lc.coop ? VR_VARIANT_COOP : 0u) | (lc.big ? VR_VARIANT_WIDE_OFFSETS : 0u) |
+                       (lc.s16 ? VR_VARIANT_STACK16 : 0u);
         // the COOP instantiations (2 waves per SIMD) keep 3 workgroups per CU (coop_grid_per_cu)
         const int per_cu = lc.coop ? coop_grid_per_cu() : grid_per_cu();
         int lr = vr::launch_render(a, lc, std::max(1, s->cu_count) * per_cu, st, mid);

@@ -244,6 +244,7 @@ struct LaunchChoice {
     int mats;         // material kinds present (bit 0 Lambertian, 1 reflective, 2 Phong / dielectric)
     bool coop;        // the cooperative-tail instantiation (RenderArgs::coop set; never with the above)
     bool big;         // 64-bit node / triangle load offsets (vr_host.cpp needs_big_offsets)
+    bool s16;         // 16-bit LDS stack entries (trees below 65,536 wide nodes; timed kernels only)
 };
 int launch_render(const RenderArgs& args, const LaunchChoice& choice, int grid_limit, void* stream,
                   void* mid_event = nullptr);

@@ -1918,11 +1918,13 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
     else if (variant == 4) VR_K(STACK, false, false, D, M, 4);  \
     else if (variant == 5 && STACK == 32) VR_K(STACK, false, false, D, M, 4, false, false, false, false, true); \
     else if (variant == 6 && STACK == 32) VR_K(STACK, false, false, D, M, 3, false, false, false, false, true); \
+    else if (s16) VR_K(STACK_S16, false, false, D, M, 3, false, false, false, false, true); \
     else VR_K(STACK, false, false, D, M, 3)
 #else
-#define VR_MODES(D, M)                                    \
-    if (recording) VR_K(STACK, false, true, D, M, 3);     \
-    else if (counting) VR_K(STACK, true, false, D, M, 3); \
+#define VR_MODES(D, M)                                                                  \
+    if (recording) VR_K(STACK, false, true, D, M, 3);                                   \
+    else if (counting) VR_K(STACK, true, false, D, M, 3);                               \
+    else if (s16) VR_K(STACK_S16, false, false, D, M, 3, false, false, false, false, true); \
     else VR_K(STACK, false, false, D, M, 3)
 #endif
     // the cooperative-tail instantiations: launches the host marks (RenderArgs::coop: small launches
@@ -1931,6 +1933,11 @@ static hipError_t launch_render_t(const RenderArgs& a, const LaunchChoice& c, in
 #define VR_COOP_MINW 2
 #endif
     const bool coop = c.coop;
+    // 16-bit LDS stack entries (LaunchChoice::s16: trees below 65,536 wide nodes) for the timed
+    // kernels of the 24 / 32 stack classes: half the stack's LDS at the same 3 waves per SIMD, C3
+    // 39.22 -> 38.71 ms, 1024^2 @64 10.83 -> 10.58 ms, records bit-identical (profiles/r06/occ)
+    constexpr int STACK_S16 = STACK <= 32 ? STACK : 32;  // (never launched for the 48 class)
+    const bool s16 = c.s16 && STACK <= 32;
     if (!c.dark0) {
         VR_MODES(false, 3);
     } else if (mats == 1) {

@@ -247,21 +247,22 @@ def trace_rays(scene, origins, directions, device=0):
 
 def render_tile_device(scene, tile: Tile, height, width, spp, seed, first_sample, state_ptr, stream_ptr=None,
                        accumulate=False, timed=False, counters=False, device=0, defer_times=False, cull=True,
-                       dist_cull=True, coop=True, lone_walk=True):
+                       dist_cull=True, coop=True, lone_walk=True, stack16=True):
     """Enqueue a render into device state records (8 f64 per pixel, vanrijn_amd/records.py) at
     `state_ptr` (a device pointer, e.g. torch.Tensor.data_ptr()).  Returns launch stats (kernel
     time when timed; `variant`: the VR_VARIANT_* bits of the kernel that ran; `defer_times`: the
     events are recorded without waiting, read by collect_launch_times; `cull=False`: every sample
     traced, VR_LAUNCH_NO_CULL; `dist_cull=False`: no BVH distance culling, VR_LAUNCH_NO_DIST_CULL;
     `coop=False`: no cooperative tail, VR_LAUNCH_NO_COOP; `lone_walk=False`: the tail's walks in
-    coop_step's per-step form only, VR_LAUNCH_NO_LONE_WALK -- all four leave the records bit-identical)."""
+    coop_step's per-step form only, VR_LAUNCH_NO_LONE_WALK; `stack16=False`: 32-bit traversal-stack
+    entries where 16-bit ones would do, VR_LAUNCH_STACK32 -- all five leave the records bit-identical)."""
     ds = _scene_handle(scene, device)
     p = _params(tile, height, width, spp, seed, first_sample, accumulate)
     st = N.LaunchStats()
     flags = (N.LAUNCH_TIMED if timed or defer_times else 0) | (N.LAUNCH_COUNTERS if counters else 0) | \
         (N.LAUNCH_DEFER_TIMES if defer_times else 0) | (0 if cull else N.LAUNCH_NO_CULL) | \
         (0 if dist_cull else N.LAUNCH_NO_DIST_CULL) | (0 if coop else N.LAUNCH_NO_COOP) | \
-        (0 if lone_walk else N.LAUNCH_NO_LONE_WALK)
+        (0 if lone_walk else N.LAUNCH_NO_LONE_WALK) | (0 if stack16 else N.LAUNCH_STACK32)
     N.check(N.lib().vr_render_tile_device(ds.handle, C.byref(p), C.c_void_p(state_ptr),
                                           C.c_void_p(stream_ptr or 0), flags, C.byref(st)))
     return st.as_dict()

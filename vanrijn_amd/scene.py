@@ -407,12 +407,14 @@ class DeviceScene:
         shading basis (VR_ERROR_SINGULAR_BASIS); -1 turns it off."""
         N.check(N.lib().vr_debug_set_fault_object(self.handle, obj))
 
-    def set_launch_flags(self, no_cull=False, no_dist_cull=False, no_coop=False, no_lone_walk=False):
+    def set_launch_flags(self, no_cull=False, no_dist_cull=False, no_coop=False, no_lone_walk=False, stack32=False):
         """Test hook (vr_debug_set_launch_flags): every later render of this scene -- per-sample
         records and host buffers included -- skips the frustum culling, the BVH distance culling or
-        the cooperative tail or its whole-walk form (each leaves the records bit-identical)."""
+        the cooperative tail or its whole-walk form, or keeps 32-bit traversal-stack entries (each
+        leaves the records bit-identical)."""
         flags = ((N.LAUNCH_NO_CULL if no_cull else 0) | (N.LAUNCH_NO_DIST_CULL if no_dist_cull else 0) |
-                 (N.LAUNCH_NO_COOP if no_coop else 0) | (N.LAUNCH_NO_LONE_WALK if no_lone_walk else 0))
+                 (N.LAUNCH_NO_COOP if no_coop else 0) | (N.LAUNCH_NO_LONE_WALK if no_lone_walk else 0) |
+                 (N.LAUNCH_STACK32 if stack32 else 0))
         N.check(N.lib().vr_debug_set_launch_flags(self.handle, flags))
 
     NODE_DTYPE = np.dtype([("box", "<f8", (2, 6)), ("child", "<i4", (2,)), ("pad", "<i4", (6,))])
