@@ -39,6 +39,8 @@ def test_bench_under_torchrun_world_one(streams):
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1 and out["steps"] == 3 and out["config"]["streams"] == streams
+    # two streams: the frames one after another are timed too (each frame's own latency)
+    assert ("sequential" in out) == (streams == 2)
     assert out["config"]["parallelism"] == "spp-split x1, RCCL reduce"
     assert out["value"] > 0 and out["ms_per_step"] > 0
     # one frame of C2 is 512 x 512 x 64 samples; value = samples / max-over-ranks time
