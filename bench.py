@@ -551,11 +551,14 @@ def main():
                     help="render the host-built traversal tree instead of the device-built one (same images)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # one profiled frame (live_pmc)
     ap.add_argument("--stub-ranks", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU, gloo)
+    # tests/test_gpu_dist_rehearsal.py: N ranks on ONE GPU (gloo, the collective on host copies of the
+    # sums) -- every step of the N-rank path but the RCCL transport, on a one-GPU box
+    ap.add_argument("--one-gpu-rehearsal", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if "RANK" not in os.environ and args.gpus > 1:  # start the ranks (nothing has touched the GPU yet)
-        return launch_ranks(sys.argv[1:], args.gpus, stub=args.stub_ranks)
+        return launch_ranks(sys.argv[1:], args.gpus, stub=args.stub_ranks or args.one_gpu_rehearsal)
     if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", 1)) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {os.environ.get('WORLD_SIZE')}: refusing to run a "
               f"different number of ranks than asked for", file=sys.stderr, flush=True)
@@ -572,7 +575,7 @@ def main():
             cfg[k] = getattr(args, k)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if args.one_gpu_rehearsal else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     # launched by torch.distributed.run (RANK set): the RCCL group is created even at world size 1,
     # so a one-GPU box rehearses the multi-GPU step (init, barriers, reduce, max-over-ranks timing)
@@ -580,7 +583,11 @@ def main():
     if distributed:
         # a generous timeout: the other ranks wait in the final barrier while rank 0 runs its PMC passes
         import datetime
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=datetime.timedelta(minutes=30))
+        if args.one_gpu_rehearsal:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=30))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(minutes=30))
         world = dist.get_world_size()  # what the line reports as n_gpus
         assert world == args.gpus, (world, args.gpus)
 
@@ -634,7 +641,7 @@ def main():
             return render_tile_device(dscene, tile, H, W, spp_r, SEED, first, st.data_ptr(), st_j.cuda_stream,
                                       timed=timed and not defer, defer_times=defer, device=local)
         with torch.cuda.stream(st_j):  # the collective, the zeroing and the timer events follow the render
-            return D.frame_step(shard, states[j], i, spp_r, timer=timer)
+            return D.frame_step(shard, states[j], i, spp_r, timer=timer, via_host=args.one_gpu_rehearsal)
 
     def timed_region(spp_r, first_step, ns=None):
         """args.warmup untimed + args.steps timed frames of spp_r samples per pixel on every rank,
@@ -666,7 +673,7 @@ def main():
             lt["max_passes"] = max(lt["max_passes"], lj["max_passes"])
         assert lt["launches"] == args.steps, lt
         if distributed:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.one_gpu_rehearsal else f"cuda:{local}")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return {"elapsed": elapsed, "kernel_s": lt["kernel_ms"] / args.steps / 1e3,
@@ -755,6 +762,9 @@ def main():
     out["scene_build"] = build
     # the path's one exchange: {sum X, Y, Z, weight} of every pixel, 32 B, reduced
     # onto rank 0 inside the timed step (RCCL; under torch.distributed.run also at world size 1)
+    if args.one_gpu_rehearsal:
+        out["rehearsal"] = (f"{world} ranks sharing ONE GPU, gloo reduce of host copies: the N-rank code path, "
+                            f"not a multi-GPU measurement")
     out["reduce"] = {"collective": "dist.reduce(SUM, f64) onto rank 0" if distributed else "none (one process)",
                      "bytes_per_step_per_rank": D.reduce_bytes(state) if distributed else 0,
                      "ms_per_step": round(sum(rccl_ms) / len(rccl_ms), 3) if rccl_ms else 0.0}

@@ -45,3 +45,27 @@ def test_bench_under_torchrun_world_one(streams):
     assert out["value"] > 0 and out["ms_per_step"] > 0
     # one frame of C2 is 512 x 512 x 64 samples; value = samples / max-over-ranks time
     assert abs(out["value"] - 512 * 512 * 64 / (out["ms_per_step"] * 1e3)) < 1e-3 * out["value"] + 1e-3
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    """bench.py's N > 1 path end to end on the one-GPU box: `bench.py --gpus 2 --one-gpu-rehearsal`
+    starts its own torch.distributed.run (the launcher), both ranks render on cuda:0 and reduce through
+    gloo on host copies of the sums (RCCL cannot put two ranks on one GPU).  Everything else is the
+    8-GPU run's code: c3 split 128 + 128 over the ranks, two streams, the weak-scaling and sequential
+    regions, max-over-ranks timing, rank 0's PMC passes on its shard while rank 1 waits in the final
+    barrier, one JSON line."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--one-gpu-rehearsal", "--config", "c3",
+           "--width", "256", "--height", "256", "--steps", "3", "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["config"]["spp_per_gpu"] == 128
+    assert out["config"]["streams"] == 2 and "rehearsal" in out
+    assert out["weak_scaling"]["spp_per_gpu"] == 256 and out["sequential"]["streams"] == 1
+    # value: both ranks' samples over the max-over-ranks time
+    assert abs(out["value"] - 2 * 256 * 256 * 128 / (out["ms_per_step"] * 1e3)) < 1e-3 * out["value"] + 1e-3
+    assert out["reduce"]["bytes_per_step_per_rank"] == 256 * 256 * 32
+    assert "shard" in out["roofline"] and out["roofline"].get("frac") is not None  # rank 0's PMC passes ran

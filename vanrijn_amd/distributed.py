@@ -45,7 +45,7 @@ def reduce_bytes(state: torch.Tensor):
     return R.sums(state).numel() * state.element_size()
 
 
-def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None, keep_local=False):
+def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None, keep_local=False, via_host=False):
     """Sum per-rank accumulation records onto `dst` (in place; the one exchange of the path).
 
     Only the merge-exact sums {sum X, sum Y, sum Z, weight} travel -- 32 B per pixel, the records'
@@ -61,7 +61,9 @@ def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None, keep_loca
     keep accumulating on every rank pass `keep_local=True`: the collective then runs on a copy of
     the sums half (32 B per pixel more HBM traffic), and the non-dst ranks' records stay their own.
     `timer`: a list that receives (start, end) CUDA events around everything this call enqueues (the
-    collective and the zeroing)."""
+    collective and the zeroing).  `via_host`: the collective runs on a host copy of the sums half
+    (a gloo group over device records: bench.py's one-GPU rehearsal of the N-rank path), the
+    result copied back on `dst`."""
     rank, world = world_info(group)
     # through the collective whenever a group exists (at world size 1 too: bench.py under
     # torch.distributed.run on one GPU rehearses the RCCL step the 8-GPU runs take)
@@ -73,7 +75,13 @@ def reduce_records(state: torch.Tensor, dst=0, group=None, timer=None, keep_loca
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         buf = sums.clone() if keep_local and rank != dst else sums
-        dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if via_host and buf.is_cuda:
+            host = buf.cpu()
+            dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            if rank == dst:
+                buf.copy_(host)
+        else:
+            dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
         if rank == dst:
             R.compensations(flat).zero_()
         if ev is not None:
@@ -89,7 +97,8 @@ def mean_colour(state: torch.Tensor):
     return torch.where(w != 0, s[:, 0:3] * (1.0 / w), torch.zeros_like(s[:, 0:3]))
 
 
-def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=None, keep_local=False):
+def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=None, keep_local=False,
+               via_host=False):
     """One frame on this rank: render_shard(first_sample, state) renders (or enqueues) this rank's
     `spp` samples per pixel into `state` (fresh records), then the records are reduced onto rank 0.
     Afterwards only rank 0's `state` is valid (the other ranks' sums half was the collective's
@@ -97,5 +106,5 @@ def frame_step(render_shard, state: torch.Tensor, step, spp, group=None, timer=N
     on the GPU)."""
     rank, world = world_info(group)
     out = render_shard(first_sample(step, rank, world, spp), state)
-    reduce_records(state, group=group, timer=timer, keep_local=keep_local)
+    reduce_records(state, group=group, timer=timer, keep_local=keep_local, via_host=via_host)
     return out
