@@ -7,6 +7,7 @@ instantiation, which has none of these, so here the product's own image path is 
 oracle on whole BASELINE frames:
 
   * C3: the main.rs scene's full 1024x1024 frame at 16 spp (16.8 M samples);
+  * C4: its full 2048x2048 frame at 4 spp (the frame's last samples, 1020..1023);
   * C5: the 1,051,392-triangle scene's full 4096x4096 frame at 1 spp (16.8 M samples);
   * a scene where the reference produces NaN: main.rs's scene plus a mesh loaded from an OBJ
     without normals (mesh.rs:37 gives it zero normals, so every hit on it has a NaN shading basis,
@@ -61,6 +62,20 @@ def test_c3_full_frame_16spp(oracle):
     nans, err = _compare_images(gpu, ref, 16, (1024, 1024))
     assert nans == 0
     print(f"C3 full frame @16 spp: max per-pixel XYZ L2 error {err:.3e}")
+
+
+def test_c4_full_frame_4spp(oracle):
+    """C4's frame size (BASELINE configs[3]: 2048x2048, the main.rs scene) in full at 4 spp (16.8 M
+    samples) -- until round 6 only a 64x64 crop of it was checked."""
+    s = scenes.main_scene()
+    ds = s.device_scene(0)
+    t = Tile(0, 2048, 0, 2048)
+    gpu = render_tile(ds, t, 2048, 2048, 4, seed=SEED, first_sample=1020)
+    ref = oracle.OracleScene(s.spec()).render_tile(t, 2048, 2048, 4, seed=SEED, first_sample=1020,
+                                                   mode=oracle.MODE_PRUNED, nthreads=THREADS)
+    nans, err = _compare_images(gpu, ref, 4, (2048, 2048))
+    assert nans == 0
+    print(f"C4 full frame @4 spp (samples 1020..1023): max per-pixel XYZ L2 error {err:.3e}")
 
 
 def test_c5_full_frame_1spp(oracle):
