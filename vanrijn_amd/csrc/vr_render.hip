@@ -117,6 +117,9 @@ constexpr int kPrioA = 0, kPrioNode = 1, kPrioLeaf = 1;
 #ifndef VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
 #define VR_WATCHDOG 0
 #endif
+#ifndef VR_NODE_STEPS  // node steps per phase-B iteration (round 6: 2)
+#define VR_NODE_STEPS 2
+#endif
 constexpr int kPend = 8;  // FIFO entries per lane of a wave, on average
 constexpr int kWaveList = 64 * kPend;
 static_assert((kWaveList & (kWaveList - 1)) == 0, "the wave FIFO is a power-of-two ring");
@@ -1369,108 +1372,122 @@ __global__ __launch_bounds__(256, MINW) void render_kernel(RenderArgs A, const P
                 const int n = VR_ROOM ? __popcll(lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) : 0;
                 if (first_active_lane()) step_hist[n == 0 ? 0 : 1 + (n - 1) / 8]++;
             }
-            if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
-                VR_MARK("node_step");
-                // 32-bit byte offset from the scalar base (node < 2^25 unless BIG): the load's saddr form,
-                // no 64-bit address arithmetic per step
-                const Node4& nd = node_at(node);
-                if (COUNT) cnt.node_visits++;
-                int c[4];
-                float f[4];
-                // per-child bits: descend / queue (f32 hit or too close to call, not culled), and
-                // too close to call.  An interior child too close to call is descended: its box is
-                // a superset of its leaves' boxes, so walking it only costs work (DESIGN.md section
-                // 5); a leaf child too close to call is queued with bit 31 set and its exact f64 box
-                // test runs in the leaf round, beside the triangle test (the f32 bounds tlo / thi
-                // enclose the exact interval either way, so the f32 cull stays conservative)
-                uint32_t hm = 0, xm = 0;
+            // VR_NODE_STEPS (2) node steps per iteration: the second, with its leaf append, before the
+            // leaf-round check, the next-BVH step and the loop condition, for the lanes still at a node
+            // while the FIFO has room -- half the iterations' bookkeeping (round 6: C3 38.96 -> 38.13 ms,
+            // C5 2048^2 @16 17.16 -> 16.34 ms, C2 -3.6 %; 3 steps: C3 38.24, C5 16.12 ms;
+            // profiles/r06/steps/).  The order of node visits and leaf tests changes, the records do not
+            // (every step and leaf round is order-independent)
+            for (int nst = 0; nst < VR_NODE_STEPS; ++nst) {
+                if (nst > 0) {
+                    if (coop || (lanes_ieq(state, kTraversing) & lanes_ige(node, 0)) == 0 || !VR_ROOM) break;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    c[k] = nd.child[k];
-                    float g;
-                    bool maybe, sure;
-                    slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
-                    const bool live = c[k] != kEmptyChild;
-                    if (COUNT && live) cnt.box_tests++;
-                    const bool pass = live && maybe && !(f[k] > cull_far || g < cull_behind);
-                    hm |= pass ? 1u << k : 0u;
-                    xm |= (pass && !sure) ? 1u << k : 0u;
+                    for (int k = 0; k < 4; ++k) lq[k] = false;
+                    if (COUNT && first_active_lane()) cnt.trav_slots += 64;
                 }
-                // leaf children: their triangles go to the wave FIFO, appended after the step by all
-                // lanes at once
-                // interior children near-first: one 32-bit key per child, the entry distance's high
-                // bits (clamped below at 0: non-negative f32 bits order like the values) over the
-                // child's node index (A.sort_mask: the low bits, wide enough for every wide node), so
-                // the sorting network is integer min / max and the index rides along; 0xffffffff
-                // (or any key with bit 31 set) marks "not descended".  Only the visiting order depends on the key.
-                const uint32_t smask = A.sort_mask;
-                uint32_t key[4];
+                if (!coop && state == kTraversing && node >= 0 && VR_ROOM) {
+                    VR_MARK("node_step");
+                    // 32-bit byte offset from the scalar base (node < 2^25 unless BIG): the load's saddr form,
+                    // no 64-bit address arithmetic per step
+                    const Node4& nd = node_at(node);
+                    if (COUNT) cnt.node_visits++;
+                    int c[4];
+                    float f[4];
+                    // per-child bits: descend / queue (f32 hit or too close to call, not culled), and
+                    // too close to call.  An interior child too close to call is descended: its box is
+                    // a superset of its leaves' boxes, so walking it only costs work (DESIGN.md section
+                    // 5); a leaf child too close to call is queued with bit 31 set and its exact f64 box
+                    // test runs in the leaf round, beside the triangle test (the f32 bounds tlo / thi
+                    // enclose the exact interval either way, so the f32 cull stays conservative)
+                    uint32_t hm = 0, xm = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const bool h = (hm >> k) & 1u;
-                    lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
-                    lq[k] = h && c[k] < 0;
-                    // a leaf or empty child's index is negative: its key has bit 31 set as it is
-                    // (negative distances, -0 and negative NaNs clamp to 0 as integers; +inf and
-                    // positive NaNs keep bit 31 clear: a hit child is never dropped)
-                    uint32_t kb = ((uint32_t)max(__float_as_int(f[k]), 0) & ~smask) | (uint32_t)c[k];
-                    asm volatile("" : "+v"(kb));  // computed for every lane: a select, not a branch
-                    key[k] = h ? kb : 0xffffffffu;
-                }
-                auto cas = [&](int i, int j) {
-                    const uint32_t ki = key[i], kj = key[j];
-                    key[i] = ki < kj ? ki : kj;
-                    key[j] = ki < kj ? kj : ki;
-                };
-                cas(0, 1);
-                cas(2, 3);
-                cas(0, 2);
-                cas(1, 3);
-                cas(1, 2);
-                if (key[0] < 0x80000000u) {
-                    // farthest first, so the nearest remaining pops first (writes at sp are
-                    // unconditional: the stack holds one spare entry)
-                    // (sp advances by 1 + (key >> 31 arithmetic): 1 for a descended child, 0 else)
-                    int32_t adv[4];
-#pragma unroll
-                    for (int k = 1; k < 4; ++k) {
-                        adv[k] = (int32_t)key[k] >> 31;
-                        asm volatile("" : "+v"(adv[k]));  // keeps the shift: LLVM would rebuild it as not + shift
+                    for (int k = 0; k < 4; ++k) {
+                        c[k] = nd.child[k];
+                        float g;
+                        bool maybe, sure;
+                        slab32_flags(nd.box[k], pre32, f[k], g, maybe, sure);
+                        const bool live = c[k] != kEmptyChild;
+                        if (COUNT && live) cnt.box_tests++;
+                        const bool pass = live && maybe && !(f[k] > cull_far || g < cull_behind);
+                        hm |= pass ? 1u << k : 0u;
+                        xm |= (pass && !sure) ? 1u << k : 0u;
                     }
-                    st_node[sp * 256 + tid] = key[3] & smask;
-                    sp += 1 + adv[3];
-                    st_node[sp * 256 + tid] = key[2] & smask;
-                    sp += 1 + adv[2];
-                    st_node[sp * 256 + tid] = key[1] & smask;
-                    sp += 1 + adv[1];
-                    node = (int)(key[0] & smask);
-                } else if (sp > 0) {
-                    --sp;
-                    node = (int)st_node[sp * 256 + tid];
-                } else {
-                    node = -1;  // this BVH is walked; its pending leaves remain
-                }
-            }
-            VR_STAMP(3);
-            VR_MARK("leaf_check");
-            __builtin_amdgcn_s_setprio(kPrioLeaf);
-            // append this step's leaves to the wave FIFO in (child slot, lane) order (skipped when no
-            // lane met a leaf: main -1.3 %, C5 -4.5 %)
-            const uint64_t lqm[4] = {__ballot(lq[0]), __ballot(lq[1]), __ballot(lq[2]), __ballot(lq[3])};
-            if ((lqm[0] | lqm[1] | lqm[2] | lqm[3]) != 0)
+                    // leaf children: their triangles go to the wave FIFO, appended after the step by all
+                    // lanes at once
+                    // interior children near-first: one 32-bit key per child, the entry distance's high
+                    // bits (clamped below at 0: non-negative f32 bits order like the values) over the
+                    // child's node index (A.sort_mask: the low bits, wide enough for every wide node), so
+                    // the sorting network is integer min / max and the index rides along; 0xffffffff
+                    // (or any key with bit 31 set) marks "not descended".  Only the visiting order depends on the key.
+                    const uint32_t smask = A.sort_mask;
+                    uint32_t key[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool lh = lq[k];
-                const uint64_t m = lqm[k];
-                if (lh) {
-                    const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
-                    wl_tri[wbase + pos] = lent[k];
-                    wl_own[wbase + pos] = (uint8_t)lane;
+                    for (int k = 0; k < 4; ++k) {
+                        const bool h = (hm >> k) & 1u;
+                        lent[k] = (~c[k]) | (((xm >> k) & 1u) ? INT32_MIN : 0);
+                        lq[k] = h && c[k] < 0;
+                        // a leaf or empty child's index is negative: its key has bit 31 set as it is
+                        // (negative distances, -0 and negative NaNs clamp to 0 as integers; +inf and
+                        // positive NaNs keep bit 31 clear: a hit child is never dropped)
+                        uint32_t kb = ((uint32_t)max(__float_as_int(f[k]), 0) & ~smask) | (uint32_t)c[k];
+                        asm volatile("" : "+v"(kb));  // computed for every lane: a select, not a branch
+                        key[k] = h ? kb : 0xffffffffu;
+                    }
+                    auto cas = [&](int i, int j) {
+                        const uint32_t ki = key[i], kj = key[j];
+                        key[i] = ki < kj ? ki : kj;
+                        key[j] = ki < kj ? kj : ki;
+                    };
+                    cas(0, 1);
+                    cas(2, 3);
+                    cas(0, 2);
+                    cas(1, 3);
+                    cas(1, 2);
+                    if (key[0] < 0x80000000u) {
+                        // farthest first, so the nearest remaining pops first (writes at sp are
+                        // unconditional: the stack holds one spare entry)
+                        // (sp advances by 1 + (key >> 31 arithmetic): 1 for a descended child, 0 else)
+                        int32_t adv[4];
+#pragma unroll
+                        for (int k = 1; k < 4; ++k) {
+                            adv[k] = (int32_t)key[k] >> 31;
+                            asm volatile("" : "+v"(adv[k]));  // keeps the shift: LLVM would rebuild it as not + shift
+                        }
+                        st_node[sp * 256 + tid] = key[3] & smask;
+                        sp += 1 + adv[3];
+                        st_node[sp * 256 + tid] = key[2] & smask;
+                        sp += 1 + adv[2];
+                        st_node[sp * 256 + tid] = key[1] & smask;
+                        sp += 1 + adv[1];
+                        node = (int)(key[0] & smask);
+                    } else if (sp > 0) {
+                        --sp;
+                        node = (int)st_node[sp * 256 + tid];
+                    } else {
+                        node = -1;  // this BVH is walked; its pending leaves remain
+                    }
                 }
-                q_tail += (uint32_t)__popcll(m);
-                np += lh ? 1 : 0;
+                VR_STAMP(3);
+                VR_MARK("leaf_check");
+                __builtin_amdgcn_s_setprio(kPrioLeaf);
+                // append this step's leaves to the wave FIFO in (child slot, lane) order (skipped when no
+                // lane met a leaf: main -1.3 %, C5 -4.5 %)
+                const uint64_t lqm[4] = {__ballot(lq[0]), __ballot(lq[1]), __ballot(lq[2]), __ballot(lq[3])};
+                if ((lqm[0] | lqm[1] | lqm[2] | lqm[3]) != 0)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool lh = lq[k];
+                    const uint64_t m = lqm[k];
+                    if (lh) {
+                        const uint32_t pos = (q_tail + (uint32_t)lanes_below(m)) & (kWaveList - 1);
+                        wl_tri[wbase + pos] = lent[k];
+                        wl_own[wbase + pos] = (uint8_t)lane;
+                    }
+                    q_tail += (uint32_t)__popcll(m);
+                    np += lh ? 1 : 0;
+                }
+                q_tail = __builtin_amdgcn_readfirstlane(q_tail);
             }
-            q_tail = __builtin_amdgcn_readfirstlane(q_tail);
             // leaf round: leaf_threshold (64) queued leaves -- every lane busy --, or enough lanes (or
             // all) are stalled on theirs
             const uint32_t queued = q_tail - q_head;
