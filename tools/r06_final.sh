@@ -3,7 +3,7 @@
 # baseline, drop-in), c1 / c2 / c5 lines, rocprofv3 kernel statistics of the c3 bench
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=${OUT:-gpurun_out/r06g}
+O=${OUT:-gpurun_out/r06j}
 mkdir -p "$O"
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/gpu_tests.log" 2>&1 || { echo "tests rc=$?"; tail -30 "$O/gpu_tests.log"; exit 1; }
