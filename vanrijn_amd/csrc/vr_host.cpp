@@ -1115,8 +1115,6 @@ vr::RenderArgs make_args(const vr_scene* s, const vr_render_params* p, double* s
         while (m < s->wide_count + 1 && m != 0xffffffffu) m = m << 1 | 1;
         a.sort_mask = m;
     }
-
-
     // block-major work items over the live blocks in Z-order (round 5): the waves in flight share a
     // compact patch of the image, so their camera rays and first hits walk the same part of the
     // tree -- C3 -4.5 %, C2 -4.5 %, C5 -4.2 %; scenes with a reflective material keep sample-major
