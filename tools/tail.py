@@ -1,7 +1,8 @@
 """Small-frame tail diagnostic: for one launch, the kernel time, the workgroup
 timeline of the counting variant (s_memrealtime at 100 MHz) and the path-length distribution of the
 same samples (record variant), so the tail can be attributed to long paths or to the launch shape.
-    python tools/tail.py <scene main|bench> <size> <spp>  -> one JSON line"""
+    VR_LIBRARY=abx/libtune.so python tools/tail.py <scene main|bench> <size> <spp>  -> one JSON line
+(VR_WG_TIMES_PATH is read only by a tuning build: OUTDIR=abx bash tools/build_variant.sh tune -DVR_TUNING_VARIANTS)"""
 import json
 import os
 import sys

@@ -1,5 +1,7 @@
 """Workgroup timeline of one render launch (counting variant, s_memrealtime at 100 MHz):
-how much of the kernel's wall time is the tail where few workgroups remain."""
+how much of the kernel's wall time is the tail where few workgroups remain.  Needs a tuning build
+(VR_WG_TIMES_PATH is read only there):  OUTDIR=abx bash tools/build_variant.sh tune -DVR_TUNING_VARIANTS;
+    VR_LIBRARY=abx/libtune.so python tools/wg_tail.py [spp] [scene] [size]"""
 import json
 import os
 import sys
