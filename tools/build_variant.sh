@@ -5,7 +5,7 @@ set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 OUT=$(mktemp -d)
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall"
+FLAGS="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Xarch_device -mllvm=-amdgpu-use-amdgpu-trackers"
 pids=()
 for s in vr_render.hip vr_image.hip vr_build.hip vr_host.cpp; do
   /opt/rocm/bin/hipcc $FLAGS "$@" -c vanrijn_amd/csrc/$s -o $OUT/${s%.*}.o &
