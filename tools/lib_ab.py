@@ -26,13 +26,15 @@ def main():
     st = torch.zeros(size * size * 8, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     render_tile_device(ds, t, size, size, spp, 1, 0, st.data_ptr(), s, timed=True)
-    ms = []
+    ms, red = [], []
     for _ in range(reps):
         r = render_tile_device(ds, t, size, size, spp, 1, 0, st.data_ptr(), s, timed=True)
         ms.append(r["kernel_ms"])
+        red.append(r["reduce_ms"])
     digest = hashlib.sha256(st.cpu().view(torch.int64).numpy().tobytes()).hexdigest()[:16]
     print(json.dumps({"lib": os.environ.get("VR_LIBRARY", "in-tree"), "scene": which, "size": size, "spp": spp,
                       "median_ms": round(statistics.median(ms), 3), "all": [round(x, 3) for x in ms],
+                      "reduce_ms": round(statistics.median(red), 3),
                       "variant": r["variant"], "digest": digest}), flush=True)
 
 

@@ -15,11 +15,13 @@ python3 - "$O/ab.jsonl" <<'PY'
 import json, sys, collections, statistics
 rows = [json.loads(l) for l in open(sys.argv[1])]
 g = collections.defaultdict(list)
+red = collections.defaultdict(list)
 dig = collections.defaultdict(set)
 for r in rows:
     k = (r["scene"], r["size"], r["spp"])
     g[(k, r["lib"])].append(r["median_ms"])
+    red[(k, r["lib"])].append(r.get("reduce_ms", 0.0))
     dig[k].add(r["digest"])
 for (k, lib), v in sorted(g.items()):
-    print(k, lib, round(statistics.mean(v), 3), [round(x, 2) for x in v], "digests equal" if len(dig[k]) == 1 else "DIGESTS DIFFER")
+    print(k, lib, round(statistics.mean(v), 3), [round(x, 2) for x in v], "reduce", round(statistics.mean(red[(k, lib)]), 3), "digests equal" if len(dig[k]) == 1 else "DIGESTS DIFFER")
 PY

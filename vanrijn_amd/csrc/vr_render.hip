@@ -113,7 +113,11 @@ __host__ __device__ inline uint64_t render_items(const RenderArgs& a, uint64_t p
 // cooperative tail, the partial child sort, plain staging stores) were removed from the source in
 // round 4; their code is kept as a patch (profiles/r04/removed_experiments.patch) and their A/B
 // numbers in DESIGN.md.
-constexpr int kPrioA = 0, kPrioNode = 1, kPrioLeaf = 1;
+#ifndef VR_PRIO  // phase A, node step, leaf round (A/B builds: -DVR_PRIO=0,2,1 ...)
+#define VR_PRIO 0, 1, 1
+#endif
+constexpr int kPrio[3] = {VR_PRIO};
+constexpr int kPrioA = kPrio[0], kPrioNode = kPrio[1], kPrioLeaf = kPrio[2];
 #ifndef VR_WATCHDOG  // debug builds: a wave stuck in phase B prints its lanes' state and stops
 #define VR_WATCHDOG 0
 #endif
